@@ -1,0 +1,137 @@
+/*
+ * pac_gpu.h -- C-ABI of the MI355X (gfx950) PAC/WAK encoder, libpacgpu.so.
+ *
+ * Drop-in boundary for the reference's per-block encode path
+ * (wisamreid/Perceptual-Audio-Codec).  Plain C types only; no torch types.
+ * Every entry point names the reference interface it replaces.  Built by
+ * perceptual-audio-codec_amd/build.py (hipcc --offload-arch=gfx950).
+ *
+ * Conventions: every int-returning function returns PAC_OK (0) or a negative
+ * PAC_E_* code; pac_last_error() then holds a thread-local message.  A context
+ * is bound to one device and one HIP stream and is not thread-safe; use one
+ * context per device / host thread (pacfile.py's encoder is single-threaded).
+ */
+#ifndef PAC_GPU_H
+#define PAC_GPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PAC_OK 0
+#define PAC_E_ARG (-1)          /* bad argument (reference: raise / assert)          */
+#define PAC_E_HIP (-2)          /* HIP runtime failure                               */
+#define PAC_E_NOMEM (-3)        /* device or host allocation failed                  */
+#define PAC_E_UNSUPPORTED (-4)  /* parameter outside what the reference encoder does */
+#define PAC_E_TABLES (-5)       /* Huffman table image missing or malformed          */
+#define PAC_E_CAPACITY (-6)     /* output buffer too small                           */
+
+/* Coder variants of the reference repository:
+ *  ORIGIN: PerceptualAudioCodec_Origin/codec/ (per-channel, no M/S, .pac)
+ *  MASTER: codec/ (M/S decision, Huffman, bit reservoir, .wak)             */
+#define PAC_PROFILE_ORIGIN 0
+#define PAC_PROFILE_MASTER 1
+
+typedef struct pac_ctx pac_ctx;
+
+/* CodingParams attribute bag (audiofile.py:51-53) as set by the driver
+ * (pacfile.py:452-461 / Origin pacfile.py:391-398). */
+typedef struct {
+    int32_t sample_rate;            /* codingParams.sampleRate                 */
+    int32_t n_channels;             /* codingParams.nChannels (master: 2)      */
+    int32_t n_mdct_lines;           /* codingParams.nMDCTLines (1024)          */
+    int32_t n_scale_bits;           /* codingParams.nScaleBits (4)             */
+    int32_t n_mant_size_bits;       /* codingParams.nMantSizeBits (4)          */
+    int32_t n_table_id_bits;        /* codingParams.nTableIDBits (4, master)   */
+    double target_bits_per_sample;  /* codingParams.targetBitsPerSample (2.27) */
+    int32_t profile;                /* PAC_PROFILE_*                           */
+    int32_t reserved;
+} pac_params;
+
+/* Cross-block encoder state of one stream: codingParams.extraBits
+ * (codec.py:229,260) and huffman.bitDeposit (Huffman.py:262,353-371).
+ * priorBlock (pacfile.py:265-268,282) is implicit in the stream's PCM. */
+typedef struct {
+    int64_t extra_bits;
+    int64_t bit_deposit;
+} pac_stream_state;
+
+/* Per-kernel device time of the last encode call (HIP events), ms. */
+typedef struct {
+    float front_ms;     /* masking-threshold + MDCT front end (dominant) */
+    float alloc_ms;     /* bit allocation                                */
+    float scan_ms;      /* byte-offset scan                              */
+    float pack_ms;      /* quantize + bit packing                        */
+    float total_ms;     /* first to last event                           */
+    int64_t n_channel_blocks;
+    int64_t out_bytes;
+} pac_timing;
+
+/* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */
+typedef struct {
+    int32_t n_channels;
+    int32_t overall[8];          /* overallScaleFactor[iCh]                     */
+    int32_t ba[8][25];           /* bitAlloc[iCh][iBand]                        */
+    int32_t sf[8][25];           /* scaleFactor[iCh][iBand]                     */
+    int32_t mant[8][1024];       /* signed mantissa code by MDCT line (0 if ba=0) */
+    int32_t table_id[8];         /* tableID[iCh] (master)                       */
+    int32_t lrms[25];            /* LRMS[iBand] (master)                        */
+    int32_t nbytes[8];           /* payload bytes of the channel-block          */
+    double smr[8][25];           /* SMR fed to BitAlloc                         */
+} pac_block_fields;
+
+/* --- context ------------------------------------------------------------ */
+int pac_ctx_create(int device, pac_ctx **out);
+void pac_ctx_destroy(pac_ctx *ctx);
+const char *pac_last_error(void);
+int pac_version(void);
+
+/* Huffman() constructor (Huffman.py:256-262): the 10 static tables, as the
+ * neutral image data/huffman_tables.bin ("PACHUF01"). Required for MASTER. */
+int pac_huffman_load(pac_ctx *ctx, const uint8_t *image, int64_t len);
+
+/* ScaleFactorBands(AssignMDCTLinesFromFreqLimits(1024, fs)) (psychoac.py:124-156,
+ * 193-213): the 25 band line counts written to the file header. */
+int pac_band_layout(int32_t sample_rate, int32_t n_lines_out[25]);
+
+/* --- encode ---------------------------------------------------------------
+ * Whole streams: the PACFile.WriteDataBlock loop over every hop plus the
+ * Close() flush block (pacfile.py:273-366), for n_streams independent
+ * streams that share one pac_params.  pcm holds the streams' interleaved
+ * int16 frames back to back; frame_offsets (host, n_streams+1) delimits them.
+ * Writes each stream's data section ('<L nBytes' + payload per channel-block,
+ * the bytes after the file header) back to back into out and its extent into
+ * stream_byte_offsets (host, n_streams+1).  *_is_device: the pointer is
+ * device memory (no PCIe copy).  states (host, n_streams, MASTER only,
+ * nullable) are the reservoir in/out. */
+int pac_encode_streams(pac_ctx *ctx, const pac_params *p, int32_t n_streams,
+                       const int16_t *pcm, const int64_t *frame_offsets, int32_t pcm_is_device,
+                       uint8_t *out, int64_t out_capacity, int32_t out_is_device,
+                       int64_t *stream_byte_offsets, pac_stream_state *states);
+
+/* Upper bound of the data-section bytes pac_encode_streams can produce. */
+int64_t pac_encode_bound(const pac_params *p, int32_t n_streams, const int64_t *frame_offsets);
+
+/* One block: codec.Encode(data, codingParams[, huffman]) + the channel-block
+ * bytes PACFile.WriteDataBlock writes (pacfile.py:285-351).  full_block (host)
+ * holds n_channels x 2048 float64 signed fractions (priorBlock ++ data). */
+int pac_encode_block(pac_ctx *ctx, const pac_params *p, const double *full_block,
+                     pac_stream_state *state, uint8_t *out, int64_t out_capacity,
+                     int64_t *out_bytes, pac_block_fields *fields);
+
+/* --- device buffers, sync, timing (benchmarks; data resident in HBM) ----- */
+int pac_device_alloc(pac_ctx *ctx, int64_t bytes, void **ptr);
+int pac_device_free(pac_ctx *ctx, void *ptr);
+int pac_copy_to_device(pac_ctx *ctx, void *dst, const void *src, int64_t bytes);
+int pac_copy_to_host(pac_ctx *ctx, void *dst, const void *src, int64_t bytes);
+/* Synthetic 48 kHz-style white-noise PCM: N(0,1)*0.25*32767, rint, clip. */
+int pac_synth_white(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_samples, uint64_t seed);
+int pac_sync(pac_ctx *ctx);
+int pac_set_timing(pac_ctx *ctx, int32_t enable);
+int pac_last_timing(pac_ctx *ctx, pac_timing *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,225 @@
+"""ctypes binding of libpacgpu.so (include/pac_gpu.h).
+
+The HIP library is the only compute path: if it is missing or cannot load,
+every encode raises -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpacgpu.so")
+HUFF_PATH = os.path.join(HERE, "data", "huffman_tables.bin")
+
+PAC_OK = 0
+ERRORS = {-1: "PAC_E_ARG", -2: "PAC_E_HIP", -3: "PAC_E_NOMEM", -4: "PAC_E_UNSUPPORTED",
+          -5: "PAC_E_TABLES", -6: "PAC_E_CAPACITY"}
+
+
+class PacError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (ERRORS.get(code, code), msg))
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [("sample_rate", C.c_int32), ("n_channels", C.c_int32),
+                ("n_mdct_lines", C.c_int32), ("n_scale_bits", C.c_int32),
+                ("n_mant_size_bits", C.c_int32), ("n_table_id_bits", C.c_int32),
+                ("target_bits_per_sample", C.c_double), ("profile", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class StreamState(C.Structure):
+    _fields_ = [("extra_bits", C.c_int64), ("bit_deposit", C.c_int64)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("front_ms", C.c_float), ("alloc_ms", C.c_float), ("scan_ms", C.c_float),
+                ("pack_ms", C.c_float), ("total_ms", C.c_float),
+                ("n_channel_blocks", C.c_int64), ("out_bytes", C.c_int64)]
+
+
+class BlockFields(C.Structure):
+    _fields_ = [("n_channels", C.c_int32), ("overall", C.c_int32 * 8),
+                ("ba", (C.c_int32 * 25) * 8), ("sf", (C.c_int32 * 25) * 8),
+                ("mant", (C.c_int32 * 1024) * 8), ("table_id", C.c_int32 * 8),
+                ("lrms", C.c_int32 * 25), ("nbytes", C.c_int32 * 8),
+                ("smr", (C.c_double * 25) * 8)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libpacgpu.so (building it first if the sources are newer)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    from . import build as _build
+    if not _build.up_to_date():
+        if os.path.exists(_build.HIPCC):
+            _build.build()
+    if not os.path.exists(LIB_PATH):
+        raise PacError(-2, "libpacgpu.so missing at %s (run python -m pac_amd.build); "
+                           "there is no CPU fallback" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "pac_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "pac_ctx_destroy": (None, [vp]),
+        "pac_last_error": (C.c_char_p, []),
+        "pac_version": (C.c_int, []),
+        "pac_huffman_load": (C.c_int, [vp, C.c_char_p, i64]),
+        "pac_band_layout": (C.c_int, [i32, C.POINTER(i32)]),
+        "pac_encode_streams": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, vp,
+                                         i64, i32, C.POINTER(i64), C.POINTER(StreamState)]),
+        "pac_encode_bound": (i64, [C.POINTER(Params), i32, C.POINTER(i64)]),
+        "pac_encode_block": (C.c_int, [vp, C.POINTER(Params), vp, C.POINTER(StreamState), vp, i64,
+                                       C.POINTER(i64), C.POINTER(BlockFields)]),
+        "pac_device_alloc": (C.c_int, [vp, i64, C.POINTER(vp)]),
+        "pac_device_free": (C.c_int, [vp, vp]),
+        "pac_copy_to_device": (C.c_int, [vp, vp, vp, i64]),
+        "pac_copy_to_host": (C.c_int, [vp, vp, vp, i64]),
+        "pac_synth_white": (C.c_int, [vp, vp, i64, C.c_uint64]),
+        "pac_sync": (C.c_int, [vp]),
+        "pac_set_timing": (C.c_int, [vp, i32]),
+        "pac_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != PAC_OK:
+        msg = lib().pac_last_error()
+        raise PacError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def band_layout(sample_rate):
+    out = (C.c_int32 * 25)()
+    check(lib().pac_band_layout(int(sample_rate), out))
+    return np.array(out[:], dtype=np.int64)
+
+
+class Context:
+    """One device context (pac_ctx): stream, tables, work buffers."""
+
+    def __init__(self, device=0, huffman=True):
+        L = lib()
+        h = C.c_void_p()
+        check(L.pac_ctx_create(int(device), C.byref(h)))
+        self.h = h
+        self.L = L
+        self.device = device
+        if huffman and os.path.exists(HUFF_PATH):
+            with open(HUFF_PATH, "rb") as f:
+                img = f.read()
+            check(L.pac_huffman_load(self.h, img, len(img)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.pac_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- encode ---------------------------------------------------------
+    def encode_streams(self, params, pcm, frame_offsets, out=None, out_capacity=None,
+                       pcm_is_device=False, out_is_device=False, states=None):
+        """pcm: host int16 array (frames x channels, streams back to back) or a
+        device pointer (int) when pcm_is_device.  Returns (out, stream_offsets)."""
+        fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
+        ns = len(fo) - 1
+        fo_p = fo.ctypes.data_as(C.POINTER(C.c_int64))
+        if out is None:
+            cap = int(self.L.pac_encode_bound(C.byref(params), ns, fo_p))
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+        if isinstance(out, np.ndarray):
+            out_ptr = out.ctypes.data
+            cap = out.nbytes if out_capacity is None else out_capacity
+        else:
+            out_ptr = out
+            cap = out_capacity
+        if pcm_is_device:
+            pcm_ptr = pcm
+        else:
+            pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+            pcm_ptr = pcm.ctypes.data
+        so = np.zeros(ns + 1, dtype=np.int64)
+        st = None
+        if states is not None:
+            st = (StreamState * ns)(*states)
+        check(self.L.pac_encode_streams(self.h, C.byref(params), ns, pcm_ptr, fo_p,
+                                        int(bool(pcm_is_device)), out_ptr, int(cap),
+                                        int(bool(out_is_device)),
+                                        so.ctypes.data_as(C.POINTER(C.c_int64)),
+                                        st if st is not None else None))
+        if states is not None:
+            for i in range(ns):
+                states[i] = st[i]
+        return out, so
+
+    def encode_block(self, params, full_block, state=None):
+        fb = np.ascontiguousarray(full_block, dtype=np.float64)
+        out = np.empty(8 * 4200, dtype=np.uint8)
+        n = C.c_int64()
+        fields = BlockFields()
+        st = state if state is not None else StreamState()
+        check(self.L.pac_encode_block(self.h, C.byref(params), fb.ctypes.data, C.byref(st),
+                                      out.ctypes.data, out.nbytes, C.byref(n), C.byref(fields)))
+        return out[:n.value].tobytes(), fields, st
+
+    # --- device memory / timing -----------------------------------------
+    def alloc(self, nbytes):
+        p = C.c_void_p()
+        check(self.L.pac_device_alloc(self.h, int(nbytes), C.byref(p)))
+        return p.value
+
+    def free(self, ptr):
+        check(self.L.pac_device_free(self.h, ptr))
+
+    def to_device(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        check(self.L.pac_copy_to_device(self.h, dst, arr.ctypes.data, arr.nbytes))
+
+    def to_host(self, arr, src):
+        check(self.L.pac_copy_to_host(self.h, arr.ctypes.data, src, arr.nbytes))
+        return arr
+
+    def synth_white(self, dev_pcm, n_samples, seed):
+        check(self.L.pac_synth_white(self.h, dev_pcm, int(n_samples), int(seed)))
+
+    def sync(self):
+        check(self.L.pac_sync(self.h))
+
+    def set_timing(self, on):
+        check(self.L.pac_set_timing(self.h, int(bool(on))))
+
+    def last_timing(self):
+        t = Timing()
+        check(self.L.pac_last_timing(self.h, C.byref(t)))
+        return t
+
+
+def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27):
+    p = Params()
+    p.sample_rate = int(sample_rate)
+    p.n_channels = int(n_channels)
+    p.n_mdct_lines = 1024
+    p.n_scale_bits = 4
+    p.n_mant_size_bits = 4
+    p.n_table_id_bits = 4
+    p.target_bits_per_sample = float(target_bits_per_sample)
+    p.profile = int(profile)
+    return p

@@ -1,0 +1,570 @@
+// pac_abi.hip -- host side of libpacgpu.so: the C-ABI declared in
+// include/pac_gpu.h, constant-table generation and kernel orchestration.
+//
+// One translation unit (kernels included) so hipcc emits one gfx950 code
+// object.  Host tables are generated in float64 with libm following the
+// reference's numpy expressions, then uploaded once per sample rate.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <vector>
+
+#include "../../include/pac_gpu.h"
+#include "pac_kernels.hip"
+
+#define PAC_VERSION 100
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+
+static thread_local char g_err[512];
+
+static int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(PAC_E_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                           \
+    } while (0)
+
+extern "C" const char* pac_last_error(void) { return g_err; }
+extern "C" int pac_version(void) { return PAC_VERSION; }
+
+// ---------------------------------------------------------------------------
+// constant tables (host, float64, libm)
+// ---------------------------------------------------------------------------
+
+static const double kCbFreqLimits[PAC_NB] = {  // psychoac.py:122
+    100.0, 200.0, 300.0, 400.0, 510.0, 630.0, 770.0, 920.0, 1080.0, 1270.0,
+    1480.0, 1720.0, 2000.0, 2320.0, 2700.0, 3150.0, 3700.0, 4400.0, 5300.0,
+    6400.0, 7700.0, 9500.0, 12000.0, 15500.0, 24000.0};
+
+static double host_bark(double f) {  // psychoac.py:56-64
+    double khz = f / 1000.0;
+    double t2 = khz / 7.5;
+    return 13.0 * atan(khz * 0.76) + 3.5 * atan(t2 * t2);
+}
+
+static double host_thresh(double f) {  // psychoac.py:44-54
+    if (f < 10.0) f = 10.0;
+    double khz = f / 1000.0;
+    double d = khz - 3.3;
+    return 3.64 * pow(khz, -0.8) + -6.5 * exp(-0.6 * (d * d)) + 0.001 * pow(khz, 4.0);
+}
+
+// AssignMDCTLinesFromFreqLimits(1024, fs) psychoac.py:124-156
+static void host_band_layout(int fs, int32_t* out) {
+    double lower = 0.0, upper = 0.0;
+    for (int b = 0; b < PAC_NB; b++) {
+        double limit = kCbFreqLimits[b];
+        upper = (limit >= fs / 2.0) ? fs / 2.0 : limit;
+        int cnt = 0;
+        for (int k = 0; k < PAC_HALFN; k++) {
+            double f = (k + 0.5) / PAC_HALFN * (double)(fs / 2);  // Py2 int sampleRate/2
+            if (f <= upper && f > lower) cnt++;
+        }
+        out[b] = cnt;
+        lower = upper;
+    }
+}
+
+static void build_tables(int fs, PacTables* t) {
+    memset(t, 0, sizeof(*t));
+    t->sample_rate = fs;
+    host_band_layout(fs, t->nlines);
+    int acc = 0;
+    for (int b = 0; b < PAC_NB; b++) {
+        t->lower[b] = acc;
+        for (int l = acc; l < acc + t->nlines[b]; l++) t->band_of_line[l] = b;
+        acc += t->nlines[b];
+    }
+    for (int l = acc; l < PAC_HALFN; l++) t->band_of_line[l] = PAC_NB - 1;  // unreachable
+    for (int n = 0; n < PAC_N; n++) {
+        double tt = (double)n;
+        t->sine[n] = sin((tt + 0.5) * M_PI / (double)PAC_N);
+        t->hann[n] = 0.5 * (1 - cos(2.0 * (tt + 0.5) * M_PI / (double)PAC_N));
+    }
+    const double M = PAC_HALFN;
+    for (int q = 0; q < PAC_HALFN / 2; q++) {
+        double a = -M_PI * (q + 0.25) / M;
+        t->mdct_pre[q] = make_double2(cos(a), sin(a));
+        double b = -M_PI * q / M;
+        t->mdct_post[q] = make_double2(cos(b), sin(b));
+        double c = -2.0 * M_PI * q / 1024.0;
+        t->fft_tw[q] = make_double2(cos(c), sin(c));
+    }
+    for (int k = 0; k < PAC_HALFN; k++) {
+        double a = -2.0 * M_PI * k / 2048.0;
+        t->rfft_tw[k] = make_double2(cos(a), sin(a));
+    }
+    {   // mdct.py:355 post-twiddle angle, evaluated as numpy does
+        double c1 = (-2.0 * M_PI) / (double)PAC_N;
+        double c2 = c1 * 512.5;
+        for (int k = 0; k < PAC_HALFN; k++) {
+            double ph = c2 * (k + 0.5);
+            t->mdct_zero_neg[k] = (cos(ph) < 0.0 && sin(ph) >= 0.0) ? 1 : 0;
+        }
+    }
+    const int step = fs / PAC_N;  // Py2 integer division, psychoac.py:188
+    double mx = -1.0;
+    for (int k = 0; k < PAC_HALFN; k++) {
+        double f = fs / 2.0 / (double)PAC_HALFN * ((double)k + 0.5);  // psychoac.py:434
+        t->bark_line[k] = host_bark(f);
+        t->tiq[k] = pow(10.0, (host_thresh(f) - 96.0) / 10.0);
+        t->bark_bin[k] = host_bark((double)(k * step));
+        double f2 = (((double)k + 0.5) / (double)PAC_HALFN) * (fs / 2.0);  // psychoac.py:570
+        double fm = f2 < 3000. ? f2 : 3000.;
+        double v = pow(10.0, 1.25 * (1 - cos(M_PI * (fm / 3000.))) - 2.5);
+        t->mld[k] = v;
+        if (v > mx) mx = v;
+    }
+    for (int k = 0; k < PAC_HALFN; k++) t->mld[k] = t->mld[k] / mx;
+}
+
+extern "C" int pac_band_layout(int32_t sample_rate, int32_t n_lines_out[25]) {
+    if (sample_rate <= 0 || !n_lines_out) return set_err(PAC_E_ARG, "bad sample rate / pointer");
+    host_band_layout(sample_rate, n_lines_out);
+    return PAC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t want) {
+        if (want <= n) return PAC_OK;
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t cap = want + want / 4 + 64;
+        if (hipMalloc((void**)&p, cap * sizeof(T)) != hipSuccess)
+            return set_err(PAC_E_NOMEM, "hipMalloc(%zu bytes) failed", cap * sizeof(T));
+        n = cap;
+        return PAC_OK;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct pac_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::map<int, PacTables*> tables;  // device tables per sample rate
+    PacHuffTables* huff = nullptr;     // device
+    bool have_huff = false;
+    // work
+    DevBuf<double> smr, bandpeak;
+    DevBuf<uint8_t> overall, ba, sf;
+    DevBuf<int32_t> nbytes;
+    DevBuf<int64_t> off, tile_sums, grand_total, frame_off, blk_off, stream_off;
+    DevBuf<int16_t> pcm_stage;
+    DevBuf<uint8_t> out_stage;
+    DevBuf<double> fsrc;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    pac_timing last = {};
+};
+
+extern "C" int pac_ctx_create(int device, pac_ctx** out) {
+    if (!out) return set_err(PAC_E_ARG, "null out");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return set_err(PAC_E_ARG, "device %d out of range (%d)", device, n);
+    HIPCHK(hipSetDevice(device));
+    pac_ctx* c = new pac_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_err(PAC_E_HIP, "hipStreamCreate failed");
+    }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    *out = c;
+    return PAC_OK;
+}
+
+extern "C" void pac_ctx_destroy(pac_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto& kv : c->tables) hipFree(kv.second);
+    if (c->huff) hipFree(c->huff);
+    c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release();
+    c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
+    c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
+    c->stream_off.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
+    for (auto& e : c->ev) hipEventDestroy(e);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int get_tables(pac_ctx* c, int fs, PacTables** out) {
+    auto it = c->tables.find(fs);
+    if (it != c->tables.end()) {
+        *out = it->second;
+        return PAC_OK;
+    }
+    PacTables* h = (PacTables*)malloc(sizeof(PacTables));
+    if (!h) return set_err(PAC_E_NOMEM, "host tables");
+    build_tables(fs, h);
+    PacTables* d = nullptr;
+    if (hipMalloc((void**)&d, sizeof(PacTables)) != hipSuccess) {
+        free(h);
+        return set_err(PAC_E_NOMEM, "device tables");
+    }
+    hipError_t e = hipMemcpy(d, h, sizeof(PacTables), hipMemcpyHostToDevice);
+    free(h);
+    if (e != hipSuccess) return set_err(PAC_E_HIP, "table upload: %s", hipGetErrorString(e));
+    c->tables[fs] = d;
+    *out = d;
+    return PAC_OK;
+}
+
+extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
+    if (!c || !buf) return set_err(PAC_E_ARG, "null argument");
+    if (len < 12 || memcmp(buf, "PACHUF01", 8) != 0) return set_err(PAC_E_TABLES, "not a PACHUF01 image");
+    uint32_t n;
+    memcpy(&n, buf + 8, 4);
+    if (n != PAC_NTAB) return set_err(PAC_E_TABLES, "expected %d tables, image has %u", PAC_NTAB, n);
+    PacHuffTables* h = (PacHuffTables*)calloc(1, sizeof(PacHuffTables));
+    if (!h) return set_err(PAC_E_NOMEM, "host huffman tables");
+    int64_t o = 12;
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t hdr[4];
+        if (o + 16 > len) { free(h); return set_err(PAC_E_TABLES, "truncated image"); }
+        memcpy(hdr, buf + o, 16);
+        o += 16;
+        uint32_t tid = hdr[0];
+        if (tid < 1 || tid > PAC_NTAB || hdr[2] < 1 || hdr[2] > 32) {
+            free(h);
+            return set_err(PAC_E_TABLES, "bad table header");
+        }
+        h->esc_len[tid - 1] = (int32_t)hdr[2];
+        h->esc_bits[tid - 1] = hdr[3];
+        for (uint32_t e = 0; e < hdr[1]; e++) {
+            int32_t sym;
+            uint32_t l, b;
+            if (o + 12 > len) { free(h); return set_err(PAC_E_TABLES, "truncated image"); }
+            memcpy(&sym, buf + o, 4);
+            memcpy(&l, buf + o + 4, 4);
+            memcpy(&b, buf + o + 8, 4);
+            o += 12;
+            if (sym < 0 || sym >= PAC_NSYM || l < 1 || l > 32) {
+                free(h);
+                return set_err(PAC_E_TABLES, "bad table entry");
+            }
+            h->len[tid - 1][sym] = (uint8_t)l;
+            h->bits[tid - 1][sym] = b;
+        }
+    }
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->huff && hipMalloc((void**)&c->huff, sizeof(PacHuffTables)) != hipSuccess) {
+        free(h);
+        return set_err(PAC_E_NOMEM, "device huffman tables");
+    }
+    hipError_t e = hipMemcpy(c->huff, h, sizeof(PacHuffTables), hipMemcpyHostToDevice);
+    free(h);
+    if (e != hipSuccess) return set_err(PAC_E_HIP, "huffman upload: %s", hipGetErrorString(e));
+    c->have_huff = true;
+    return PAC_OK;
+}
+
+static int check_params(const pac_params* p) {
+    if (!p) return set_err(PAC_E_ARG, "null params");
+    if (p->n_mdct_lines != 1024 || p->n_scale_bits != 4 || p->n_mant_size_bits != 4)
+        return set_err(PAC_E_UNSUPPORTED,
+                       "only nMDCTLines=1024, nScaleBits=4, nMantSizeBits=4 (pacfile.py:452-454)");
+    if (p->sample_rate < PAC_N || p->sample_rate > 400000)
+        return set_err(PAC_E_UNSUPPORTED, "sample rate %d", p->sample_rate);
+    if (p->profile == PAC_PROFILE_ORIGIN) {
+        if (p->n_channels < 1 || p->n_channels > 8) return set_err(PAC_E_ARG, "n_channels %d", p->n_channels);
+    } else if (p->profile == PAC_PROFILE_MASTER) {
+        if (p->n_channels != 2)
+            return set_err(PAC_E_UNSUPPORTED, "master coder is stereo only (codec.py:46-47,98)");
+        if (p->n_table_id_bits != 4) return set_err(PAC_E_UNSUPPORTED, "nTableIDBits must be 4");
+    } else {
+        return set_err(PAC_E_ARG, "unknown profile %d", p->profile);
+    }
+    if (!(p->target_bits_per_sample > 0.0)) return set_err(PAC_E_ARG, "targetBitsPerSample");
+    return PAC_OK;
+}
+
+// bitBudget as codec.py:223-227 / Origin codec.py:86-88 compute it, same op order
+static double bit_budget(const pac_params* p) {
+    double b = p->target_bits_per_sample * 1024;
+    b -= p->n_scale_bits * (PAC_NB + 1);
+    b -= p->n_mant_size_bits * PAC_NB;
+    if (p->profile == PAC_PROFILE_MASTER) b -= p->n_table_id_bits;
+    return b;
+}
+
+extern "C" int64_t pac_encode_bound(const pac_params* p, int32_t n_streams, const int64_t* fo) {
+    if (!p || !fo || n_streams < 0) return -1;
+    int64_t blocks = 0;
+    for (int s = 0; s < n_streams; s++) blocks += (fo[s + 1] - fo[s] + PAC_HALFN - 1) / PAC_HALFN + 1;
+    // payload <= 4 + 25*8 + 16*1024 (+ 25 LRMS + sign bits for master) bits
+    int64_t per = 4 + (4 + 4 + 25 * 8 + 16 * 1024 + 25 + 1024 + 1024 * 16 + 7) / 8;
+    return blocks * p->n_channels * per;
+}
+
+__global__ void k_stream_offsets(const int64_t* __restrict__ off, const int64_t* __restrict__ blk_off,
+                                 int n_streams, int nch, const int64_t* __restrict__ total,
+                                 int64_t* __restrict__ so) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n_streams) so[s] = off[blk_off[s] * nch];
+    if (s == n_streams) so[s] = *total;
+}
+
+static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src, int64_t G,
+                      uint8_t* out_dev, int64_t out_cap, int64_t* out_total, int64_t** off_dev) {
+    int rc;
+    if ((rc = c->smr.ensure(PAC_NB * G)) || (rc = c->bandpeak.ensure(PAC_NB * G)) ||
+        (rc = c->overall.ensure(G)) || (rc = c->ba.ensure(PAC_NB * G)) || (rc = c->sf.ensure(PAC_NB * G)) ||
+        (rc = c->nbytes.ensure(G)) || (rc = c->off.ensure(G + 1)) ||
+        (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)))
+        return rc;
+    PacOriginWork W{c->smr.p, c->bandpeak.p, c->overall.p, c->ba.p, c->sf.p, c->nbytes.p};
+    hipStream_t s = c->stream;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
+    hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(64), 0, s, src, T, W, G);
+    HIPCHK(hipGetLastError());
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+    hipLaunchKernelGGL(k_origin_alloc, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, T, W, G,
+                       bit_budget(p), 16);
+    HIPCHK(hipGetLastError());
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
+    int64_t ntiles = (G + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G, c->tile_sums.p);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tile_sums.p, ntiles, c->grand_total.p);
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G, c->tile_sums.p,
+                       c->off.p);
+    HIPCHK(hipGetLastError());
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
+    int64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (total > out_cap) return set_err(PAC_E_CAPACITY, "output needs %lld bytes, capacity %lld",
+                                        (long long)total, (long long)out_cap);
+    hipLaunchKernelGGL(k_origin_pack, dim3((unsigned)G), dim3(64), 0, s, src, T, W, G, c->off.p, out_dev);
+    HIPCHK(hipGetLastError());
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[4], s));
+    *out_total = total;
+    *off_dev = c->off.p;
+    return PAC_OK;
+}
+
+static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
+    if (!c->timing) return;
+    hipEventSynchronize(c->ev[4]);
+    hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
+    hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
+    hipEventElapsedTime(&c->last.scan_ms, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&c->last.pack_ms, c->ev[3], c->ev[4]);
+    hipEventElapsedTime(&c->last.total_ms, c->ev[0], c->ev[4]);
+    c->last.n_channel_blocks = G;
+    c->last.out_bytes = bytes;
+}
+
+extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_streams, const int16_t* pcm,
+                                  const int64_t* frame_offsets, int32_t pcm_is_device, uint8_t* out,
+                                  int64_t out_capacity, int32_t out_is_device, int64_t* stream_byte_offsets,
+                                  pac_stream_state* states) {
+    (void)states;
+    int rc;
+    if (!c || !frame_offsets || !out || !stream_byte_offsets || n_streams < 1)
+        return set_err(PAC_E_ARG, "null argument or n_streams < 1");
+    if ((rc = check_params(p))) return rc;
+    if (p->profile != PAC_PROFILE_ORIGIN)
+        return set_err(PAC_E_UNSUPPORTED, "master profile: pac_encode_streams not built yet");
+    for (int s = 0; s < n_streams; s++)
+        if (frame_offsets[s + 1] < frame_offsets[s] || frame_offsets[0] != 0)
+            return set_err(PAC_E_ARG, "frame_offsets must start at 0 and be non-decreasing");
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    const int nch = p->n_channels;
+    std::vector<int64_t> blk(n_streams + 1);
+    blk[0] = 0;
+    for (int s = 0; s < n_streams; s++)
+        blk[s + 1] = blk[s] + (frame_offsets[s + 1] - frame_offsets[s] + PAC_HALFN - 1) / PAC_HALFN + 1;
+    const int64_t nblocks = blk[n_streams];
+    const int64_t G = nblocks * nch;
+    if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
+    const int64_t nframes = frame_offsets[n_streams];
+    hipStream_t s = c->stream;
+    if ((rc = c->frame_off.ensure(n_streams + 1)) || (rc = c->blk_off.ensure(n_streams + 1)) ||
+        (rc = c->stream_off.ensure(n_streams + 1)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(c->frame_off.p, frame_offsets, (n_streams + 1) * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->blk_off.p, blk.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    const int16_t* pcm_dev = pcm;
+    if (!pcm_is_device) {
+        if ((rc = c->pcm_stage.ensure(nframes * nch + 1))) return rc;
+        if (nframes) HIPCHK(hipMemcpyAsync(c->pcm_stage.p, pcm, nframes * nch * sizeof(int16_t),
+                                           hipMemcpyHostToDevice, s));
+        pcm_dev = c->pcm_stage.p;
+    }
+    uint8_t* out_dev = out;
+    if (!out_is_device) {
+        int64_t bound = pac_encode_bound(p, n_streams, frame_offsets);
+        int64_t want = bound < out_capacity ? bound : out_capacity;
+        if ((rc = c->out_stage.ensure(want))) return rc;
+        out_dev = c->out_stage.p;
+    }
+    PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch};
+    int64_t total = 0;
+    int64_t* off_dev = nullptr;
+    if ((rc = run_origin(c, p, T, src, G, out_dev, out_capacity, &total, &off_dev))) return rc;
+    hipLaunchKernelGGL(k_stream_offsets, dim3((n_streams + 1 + 255) / 256), dim3(256), 0, s, off_dev,
+                       c->blk_off.p, n_streams, nch, c->grand_total.p, c->stream_off.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(stream_byte_offsets, c->stream_off.p, (n_streams + 1) * sizeof(int64_t),
+                          hipMemcpyDeviceToHost, s));
+    if (!out_is_device && total) HIPCHK(hipMemcpyAsync(out, out_dev, total, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    finish_timing(c, G, total);
+    return PAC_OK;
+}
+
+// --- per-block API ----------------------------------------------------------
+
+struct BitReader {
+    const uint8_t* p;
+    int64_t bit;
+    uint32_t get(int n) {
+        uint32_t v = 0;
+        for (int i = 0; i < n; i++, bit++) v = (v << 1) | ((p[bit >> 3] >> (7 - (bit & 7))) & 1u);
+        return v;
+    }
+};
+
+extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* full_block,
+                                pac_stream_state* state, uint8_t* out, int64_t out_capacity, int64_t* out_bytes,
+                                pac_block_fields* fields) {
+    (void)state;
+    int rc;
+    if (!c || !full_block || !out || !out_bytes) return set_err(PAC_E_ARG, "null argument");
+    if ((rc = check_params(p))) return rc;
+    if (p->profile != PAC_PROFILE_ORIGIN)
+        return set_err(PAC_E_UNSUPPORTED, "master profile: pac_encode_block not built yet");
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    const int nch = p->n_channels;
+    const int64_t G = nch;
+    hipStream_t s = c->stream;
+    if ((rc = c->fsrc.ensure(G * PAC_N)) || (rc = c->out_stage.ensure(G * 4200))) return rc;
+    HIPCHK(hipMemcpyAsync(c->fsrc.p, full_block, G * PAC_N * sizeof(double), hipMemcpyHostToDevice, s));
+    PacSource src{nullptr, nullptr, nullptr, c->fsrc.p, 1, nch};
+    int64_t total = 0;
+    int64_t* off_dev = nullptr;
+    if ((rc = run_origin(c, p, T, src, G, c->out_stage.p, c->out_stage.n, &total, &off_dev))) return rc;
+    if (total > out_capacity) return set_err(PAC_E_CAPACITY, "block needs %lld bytes", (long long)total);
+    HIPCHK(hipMemcpyAsync(out, c->out_stage.p, total, hipMemcpyDeviceToHost, s));
+    std::vector<double> smr(PAC_NB * G);
+    HIPCHK(hipMemcpyAsync(smr.data(), c->smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    finish_timing(c, G, total);
+    *out_bytes = total;
+    if (fields) {
+        // reconstruct the codec.Encode() tuple from the GPU-written channel-blocks
+        memset(fields, 0, sizeof(*fields));
+        fields->n_channels = nch;
+        int32_t nl[PAC_NB];
+        host_band_layout(p->sample_rate, nl);
+        int64_t o = 0;
+        for (int ch = 0; ch < nch; ch++) {
+            uint32_t nb = out[o] | (out[o + 1] << 8) | (out[o + 2] << 16) | ((uint32_t)out[o + 3] << 24);
+            fields->nbytes[ch] = (int32_t)nb;
+            BitReader br{out + o + 4, 0};
+            fields->overall[ch] = (int32_t)br.get(4);
+            int line = 0;
+            for (int b = 0; b < PAC_NB; b++) {
+                int ba = (int)br.get(4);
+                if (ba) ba++;
+                fields->ba[ch][b] = ba;
+                fields->sf[ch][b] = (int32_t)br.get(4);
+                fields->smr[ch][b] = smr[b * G + ch];
+                for (int l = 0; l < nl[b]; l++) fields->mant[ch][line + l] = ba ? (int32_t)br.get(ba) : 0;
+                line += nl[b];
+            }
+            o += 4 + nb;
+        }
+    }
+    return PAC_OK;
+}
+
+// --- device buffers / sync / timing -----------------------------------------
+
+extern "C" int pac_device_alloc(pac_ctx* c, int64_t bytes, void** ptr) {
+    if (!c || !ptr || bytes < 0) return set_err(PAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess) return set_err(PAC_E_NOMEM, "hipMalloc(%lld)", (long long)bytes);
+    return PAC_OK;
+}
+extern "C" int pac_device_free(pac_ctx* c, void* ptr) {
+    if (!c) return set_err(PAC_E_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipFree(ptr));
+    return PAC_OK;
+}
+extern "C" int pac_copy_to_device(pac_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c) return set_err(PAC_E_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return PAC_OK;
+}
+extern "C" int pac_copy_to_host(pac_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c) return set_err(PAC_E_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return PAC_OK;
+}
+extern "C" int pac_synth_white(pac_ctx* c, int16_t* dev_pcm, int64_t n, uint64_t seed) {
+    if (!c || !dev_pcm || n < 0) return set_err(PAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_synth_white, dim3(4096), dim3(256), 0, c->stream, dev_pcm, n, seed);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return PAC_OK;
+}
+extern "C" int pac_sync(pac_ctx* c) {
+    if (!c) return set_err(PAC_E_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return PAC_OK;
+}
+extern "C" int pac_set_timing(pac_ctx* c, int32_t enable) {
+    if (!c) return set_err(PAC_E_ARG, "null ctx");
+    c->timing = enable != 0;
+    return PAC_OK;
+}
+extern "C" int pac_last_timing(pac_ctx* c, pac_timing* out) {
+    if (!c || !out) return set_err(PAC_E_ARG, "null argument");
+    *out = c->last;
+    return PAC_OK;
+}

@@ -1,0 +1,25 @@
+// pac_kernels.h -- internal kernel interface (device structs + kernel decls).
+#pragma once
+#include "pac_common.h"
+
+// Where the channel-blocks' samples come from.
+struct PacSource {
+    const int16_t* pcm;        // interleaved int16 frames of all streams (device)
+    const int64_t* frame_off;  // [n_streams+1] frame prefix (device)
+    const int64_t* blk_off;    // [n_streams+1] block prefix incl. flush block (device)
+    const double* fsrc;        // OR float64 blocks [n_blocks][n_ch][2048] (device), per-block API
+    int n_streams;
+    int n_ch;
+};
+
+// Per-channel-block work arrays (structure of arrays: index [band * G + g]).
+struct PacOriginWork {
+    double* smr;        // [25][G]
+    double* bandpeak;   // [25][G] max |scaled line| per band
+    uint8_t* overall;   // [G]
+    uint8_t* ba;        // [25][G]
+    uint8_t* sf;        // [25][G]
+    int32_t* nbytes;    // [G] 4 + payload bytes
+};
+
+#define SCAN_TILE 2048

@@ -1,0 +1,364 @@
+// pac_kernels.hip -- gfx950 kernels of the PAC encoder (origin profile).
+//
+// Pipeline for G channel-blocks (stream s, block b, channel c):
+//   k_origin_front   one wave per channel-block: sine window, MDCT, overall
+//                    scale (codec.py:237-246 / Origin codec.py:90-98), Hann
+//                    spectrum, findpeaks, masker sum, per-band SMR
+//                    (Origin psychoac.py:215-314), band peak |line|
+//   k_origin_alloc   one LANE per channel-block: greedy BitAlloc
+//                    (Origin bitalloc.py:129-202), scale factors, byte size
+//   k_scan_*         exclusive scan of channel-block byte sizes -> offsets
+//   k_origin_pack    one wave per channel-block: MDCT recomputed (cheaper
+//                    than storing 8 KB/line set), mantissas (quantize.py:315),
+//                    MSB-first bit packing into LDS (bitpack.py:36-101),
+//                    '<L nBytes' + payload (Origin pacfile.py:265-306)
+#include "pac_wave.h"
+#include "pac_kernels.h"
+
+// ---------------------------------------------------------------------------
+// sample access
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int upper_bound_i64(const int64_t* __restrict__ a, int n, int64_t v) {
+    int lo = 0, hi = n;     // first index with a[idx] > v
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+struct BlockRef {
+    const int16_t* pcm;   // first frame of the stream
+    const double* fsrc;   // float samples of this channel-block (per-block API) or null
+    int64_t first_frame;  // frame index of sample 0 = (b-1)*1024
+    int64_t n_frames;
+    int nch, c;
+};
+
+__device__ __forceinline__ BlockRef locate(const PacSource& src, int64_t gb, int c) {
+    BlockRef r;
+    r.nch = src.n_ch;
+    r.c = c;
+    if (src.fsrc) {           // per-block float path: [gb][nch][2048]
+        r.fsrc = src.fsrc + (gb * src.n_ch + c) * PAC_N;
+        r.pcm = nullptr;
+        r.first_frame = 0;
+        r.n_frames = 0;
+        return r;
+    }
+    int s = upper_bound_i64(src.blk_off, src.n_streams + 1, gb) - 1;
+    int64_t b = gb - src.blk_off[s];
+    int64_t f0 = src.frame_off[s];
+    r.pcm = src.pcm + f0 * src.n_ch;
+    r.fsrc = nullptr;
+    r.first_frame = (b - 1) * PAC_HALFN;
+    r.n_frames = src.frame_off[s + 1] - f0;
+    return r;
+}
+
+// raw signed-fraction sample i (0..2047) of the block: prior hop ++ current
+// hop (pacfile.py:279-282), zero outside the stream (pcmfile.py:77-79, the
+// zero first prior block pacfile.py:265-268 and the Close() flush block)
+__device__ __forceinline__ double sample(const BlockRef& r, int i) {
+    if (r.fsrc) return r.fsrc[i];
+    int64_t f = r.first_frame + i;
+    if (f < 0 || f >= r.n_frames) return 0.0;
+    return pac_pcm_to_float(r.pcm[f * r.nch + r.c]);
+}
+
+// ---------------------------------------------------------------------------
+// origin front: MDCT, overall scale, threshold, SMR
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
+                                                     PacOriginWork W, int64_t G) {
+    __shared__ double2 buf[1024];          // 16 KB: spectrum / masker list / MDCT scratch
+    const int lane = threadIdx.x;
+    const int64_t g = blockIdx.x;
+    const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
+
+    // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
+    auto dsh = [&](int i) { return __dmul_rn(__dmul_rn(sample(r, i), T->sine[i]), T->hann[i]); };
+    wave_spectrum_mag(dsh, T, buf, lane);
+    int nm = wave_find_maskers(buf, T, 15.0, lane);
+    double thr[16];
+    wave_masking(reinterpret_cast<const Masker*>(buf), nm, T, lane, thr);
+    wave_sync();
+
+    // --- MDCT of the sine-windowed block --------------------------------
+    double* X = reinterpret_cast<double*>(buf + 512);
+    auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
+    wave_mdct(xs, T, buf, X, lane);
+    double mx = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = fmax(mx, fabs(X[j * WAVE + lane]));
+    mx = wave_max(mx);
+    const int overall = pac_scale_factor(mx, 5);
+    const double gain = (double)(1 << overall);
+
+    // --- SMR (Origin psychoac.py:281-314): SPL(4 (X/2^s)^2) - thr ---------
+    double* d = reinterpret_cast<double*>(buf);     // 1024 doubles (first 8 KB)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        int l = j * WAVE + lane;
+        double x = X[l];                        // unscaled; (x*2^s)/2^s == x exactly
+        d[l] = pac_spl(4.0 * (x * x)) - thr[j];
+    }
+    wave_sync();
+    // band peak |line| of the SCALED lines, for the scale factors
+    if (lane < PAC_NB) {
+        int lo = T->lower[lane], n = T->nlines[lane];
+        double sm = -INFINITY, pk = 0.0;
+        for (int l = lo; l < lo + n; ++l) {
+            sm = fmax(sm, d[l]);
+            pk = fmax(pk, fabs(X[l] * gain));
+        }
+        W.smr[lane * G + g] = n ? sm : 0.0;
+        W.bandpeak[lane * G + g] = pk;
+    }
+    if (lane == 0) W.overall[g] = (uint8_t)overall;
+}
+
+// ---------------------------------------------------------------------------
+// origin bit allocation: one lane per channel-block
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_origin_alloc(const PacTables* __restrict__ T, PacOriginWork W,
+                                                      int64_t G, double bitBudget, int maxMantBits) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    double nf[PAC_NB];
+    int alloc[PAC_NB];
+    int nl[PAC_NB];
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        nf[b] = W.smr[b * G + g];
+        alloc[b] = 0;
+        nl[b] = T->nlines[b];
+    }
+    double remaining = bitBudget;
+    long counter = 0;
+    int n_ninf = 0;
+    // Origin bitalloc.py:175-194; stops early once no band can take bits any
+    // more (the remaining iterations would only lower noise floors).
+    while (remaining > 0) {
+        if (n_ninf == PAC_NB) break;
+        int im = 0;
+        double best = nf[0];
+#pragma unroll
+        for (int b = 1; b < PAC_NB; ++b)
+            if (nf[b] > best) { best = nf[b]; im = b; }
+        bool stuck = false;
+#pragma unroll
+        for (int b = 0; b < PAC_NB; ++b) {
+            if (b != im) continue;
+            if (alloc[b] < maxMantBits && (remaining - nl[b]) >= 0) {
+                alloc[b] += 1;
+                remaining -= nl[b];
+            } else if (alloc[b] >= maxMantBits) {
+                if (nf[b] != -INFINITY) n_ninf++;
+                nf[b] = -INFINITY;
+            } else {
+                stuck = true;
+            }
+            nf[b] -= 6.0;
+        }
+        counter++;
+        if ((double)counter > bitBudget) break;
+        if (stuck) {
+            bool any = false;
+#pragma unroll
+            for (int b = 0; b < PAC_NB; ++b)
+                any |= (alloc[b] < maxMantBits) && (nf[b] != -INFINITY) && (remaining - nl[b]) >= 0;
+            if (!any) break;
+        }
+    }
+    int bits = 4;
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        int a = alloc[b];
+        if (a < 2) a = 0;
+        if (a > maxMantBits) a = maxMantBits;
+        W.ba[b * G + g] = (uint8_t)a;
+        W.sf[b * G + g] = (uint8_t)pac_scale_factor(W.bandpeak[b * G + g], a);
+        bits += 8 + a * nl[b];
+    }
+    W.nbytes[g] = 4 + (bits + 7) / 8;
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan of int32 sizes -> int64 offsets (3 kernels, 2048 per tile)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int64_t block_exclusive_scan_256(int64_t v, int64_t* sh, int64_t* total) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        int64_t w = t >= o ? sh[t - o] : 0;
+        __syncthreads();
+        sh[t] += w;
+        __syncthreads();
+    }
+    int64_t incl = sh[t];
+    *total = sh[255];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_tiles(const int32_t* __restrict__ sz, int64_t n,
+                                                    int64_t* __restrict__ tile_sums) {
+    __shared__ int64_t sh[256];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    int64_t acc = 0;
+    for (int k = 0; k < SCAN_TILE / 256; ++k) {
+        int64_t i = base + k * 256 + threadIdx.x;
+        acc += i < n ? sz[i] : 0;
+    }
+    int64_t tot;
+    block_exclusive_scan_256(acc, sh, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_sums(int64_t* __restrict__ tile_sums, int64_t ntiles,
+                                                   int64_t* __restrict__ grand_total) {
+    __shared__ int64_t sh[256];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < ntiles; b0 += 256) {
+        int64_t i = b0 + threadIdx.x;
+        int64_t v = i < ntiles ? tile_sums[i] : 0;
+        int64_t tot;
+        int64_t ex = block_exclusive_scan_256(v, sh, &tot);
+        if (i < ntiles) tile_sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *grand_total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const int32_t* __restrict__ sz, int64_t n,
+                                                    const int64_t* __restrict__ tile_sums,
+                                                    int64_t* __restrict__ off) {
+    __shared__ int64_t sh[256];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    // each thread owns 8 consecutive elements
+    int64_t i0 = base + threadIdx.x * 8;
+    int64_t v[8], acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int64_t i = i0 + k;
+        v[k] = i < n ? sz[i] : 0;
+        acc += v[k];
+    }
+    int64_t tot;
+    int64_t ex = block_exclusive_scan_256(acc, sh, &tot) + tile_sums[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int64_t i = i0 + k;
+        if (i < n) off[i] = ex;
+        ex += v[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bit packing helpers (MSB-first, bitpack.py:36-101), LDS u32 words
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void put_bits(uint32_t* words, int p, uint32_t v, int w) {
+    while (w > 0) {
+        int B = p >> 3, o = p & 7;
+        int take = (8 - o) < w ? (8 - o) : w;
+        uint32_t chunk = (v >> (w - take)) & ((1u << take) - 1u);
+        uint32_t byteval = chunk << (8 - o - take);
+        atomicOr(&words[B >> 2], byteval << (8 * (B & 3)));
+        p += take;
+        w -= take;
+    }
+}
+
+__device__ __forceinline__ void store_block_bytes(uint8_t* __restrict__ out, const uint32_t* words,
+                                                  int nbytes, int lane) {
+    if (lane < 4) out[lane] = (uint8_t)((uint32_t)nbytes >> (8 * lane));   // '<L' nBytes
+    for (int i = lane; i < nbytes; i += WAVE) out[4 + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
+}
+
+#define PACK_WORDS 640   // >= (4 + 25*8 + 16*1024 + 25 + 1024)/32 bits
+
+// ---------------------------------------------------------------------------
+// origin pack: one wave per channel-block
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_origin_pack(PacSource src, const PacTables* __restrict__ T,
+                                                    PacOriginWork W, int64_t G,
+                                                    const int64_t* __restrict__ off,
+                                                    uint8_t* __restrict__ out) {
+    __shared__ double2 buf[512];
+    __shared__ double X[1024];
+    __shared__ uint32_t words[PACK_WORDS];
+    __shared__ int start[PAC_NB];
+    __shared__ int bas[PAC_NB], sfs[PAC_NB];
+    const int lane = threadIdx.x;
+    const int64_t g = blockIdx.x;
+    const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
+    for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
+    if (lane < PAC_NB) {
+        bas[lane] = W.ba[lane * G + g];
+        sfs[lane] = W.sf[lane * G + g];
+    }
+    auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
+    wave_mdct(xs, T, buf, X, lane);      // identical to the front kernel's lines
+    if (lane == 0) {
+        int p = 4;
+        for (int b = 0; b < PAC_NB; ++b) { start[b] = p; p += 8 + bas[b] * T->nlines[b]; }
+    }
+    wave_sync();
+    const int overall = W.overall[g];
+    const double gain = (double)(1 << overall);
+    if (lane == 0) put_bits(words, 0, (uint32_t)overall, 4);
+    if (lane < PAC_NB) {
+        int ba = bas[lane];
+        put_bits(words, start[lane], (uint32_t)(ba ? ba - 1 : 0), 4);
+        put_bits(words, start[lane] + 4, (uint32_t)sfs[lane], 4);
+    }
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+        int l = j * WAVE + lane;
+        int b = T->band_of_line[l];
+        int ba = bas[b];
+        if (ba) {
+            uint32_t m = pac_mantissa(X[l] * gain, sfs[b], ba);
+            put_bits(words, start[b] + 8 + (l - T->lower[b]) * ba, m, ba);
+        }
+    }
+    wave_sync();
+    const int nbytes = W.nbytes[g] - 4;
+    store_block_bytes(out + off[g], words, nbytes, lane);
+}
+
+// ---------------------------------------------------------------------------
+// synthetic input (bench): counter-hash Gaussian PCM, 48 kHz stereo config 2
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// sample n of a stream: N(0,1) * 0.25 * 32767, rounded, clipped to int16
+// (Box-Muller from two 53-bit uniforms; host mirror: pac_amd.synth.white_pcm)
+__global__ void k_synth_white(int16_t* __restrict__ pcm, int64_t n, uint64_t seed) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        uint64_t h1 = splitmix64(seed ^ (2 * (uint64_t)i));
+        uint64_t h2 = splitmix64(seed ^ (2 * (uint64_t)i + 1));
+        double u1 = ((double)(h1 >> 11) + 1.0) * 0x1.0p-53;   // (0,1]
+        double u2 = (double)(h2 >> 11) * 0x1.0p-53;           // [0,1)
+        double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        double v = __builtin_rint(z * 0.25 * 32767.0);
+        v = v > 32767.0 ? 32767.0 : (v < -32768.0 ? -32768.0 : v);
+        pcm[i] = (int16_t)v;
+    }
+}

@@ -1,0 +1,222 @@
+// pac_wave.h -- one-wavefront building blocks of the per-block encode path on
+// gfx950: radix-2 FFTs staged in LDS, the sine-window MDCT (N/4-point complex
+// FFT form of mdct.py:49-82), the Hann-window side-chain spectrum
+// (psychoac.py:428), findpeaks + masker SPL (psychoac.py:158-191, 442-449) and
+// the masking-threshold sum (psychoac.py:447-456).
+//
+// Every function here is executed by ONE 64-lane wave that owns its LDS
+// scratch; "wave sync" is __syncthreads() on a 64-thread workgroup, or a
+// wave barrier when several independent waves share a workgroup.
+#pragma once
+#include "pac_common.h"
+
+#define WAVE 64
+
+__device__ __forceinline__ void wave_sync() {
+    // LDS hand-off between lanes of one wave: drain this wave's LDS ops and
+    // keep the compiler from moving accesses across (waves never share LDS).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        double w = __shfl_xor(v, o, WAVE);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ unsigned brev(unsigned x, int bits) {
+    return __builtin_bitreverse32(x) >> (32 - bits);
+}
+
+// In-place radix-2 DIT FFT of n = 2^LOG complex values that were stored in
+// bit-reversed order.  Twiddles: tw[k] = exp(-2 pi i k / 1024), k < 512.
+template <int LOG>
+__device__ __forceinline__ void wave_fft(double2* buf, const double2* __restrict__ tw, int lane) {
+    constexpr int n = 1 << LOG;
+#pragma unroll 1
+    for (int s = 1; s <= LOG; ++s) {
+        const int half = 1 << (s - 1);
+        const int tstride = 1024 >> s;
+        wave_sync();
+#pragma unroll
+        for (int t0 = 0; t0 < n / 2; t0 += WAVE) {
+            int t = t0 + lane;
+            int k = t & (half - 1);
+            int i = ((t >> (s - 1)) << s) + k;
+            double2 w = tw[k * tstride];
+            double2 a = buf[i], b = buf[i + half];
+            double2 bw = cmul(b, w);
+            buf[i] = make_double2(__dadd_rn(a.x, bw.x), __dadd_rn(a.y, bw.y));
+            buf[i + half] = make_double2(__dsub_rn(a.x, bw.x), __dsub_rn(a.y, bw.y));
+        }
+    }
+    wave_sync();
+}
+
+// MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
+// sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
+// place in codec.py:240).  Evaluated as DCT-IV of the folded block with a
+// 512-point complex FFT.  buf: 512 double2 of LDS scratch.  Output: X[1024]
+// in LDS.
+template <class XS>
+__device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                          double2* buf, double* X, int lane) {
+#pragma unroll
+    for (int q0 = 0; q0 < 512; q0 += WAVE) {
+        int q = q0 + lane;
+        int n0 = 2 * q, n1 = 1023 - 2 * q;
+        // fold [a b c d] -> (-c_r - d, a - b_r)
+        double u0 = n0 < 512 ? __dsub_rn(-xs(1535 - n0), xs(1536 + n0))
+                             : __dsub_rn(xs(n0 - 512), xs(1535 - n0));
+        double u1 = n1 < 512 ? __dsub_rn(-xs(1535 - n1), xs(1536 + n1))
+                             : __dsub_rn(xs(n1 - 512), xs(1535 - n1));
+        buf[brev(q, 9)] = cmul(make_double2(u0, u1), T->mdct_pre[q]);
+    }
+    wave_fft<9>(buf, T->fft_tw, lane);
+#pragma unroll
+    for (int q0 = 0; q0 < 512; q0 += WAVE) {
+        int q = q0 + lane;
+        double2 y = cmul(buf[q], T->mdct_post[q]);
+        double x0 = y.x * (1.0 / 1024.0), x1 = -y.y * (1.0 / 1024.0);
+        if (x0 == 0.0) x0 = T->mdct_zero_neg[2 * q] ? -0.0 : 0.0;
+        if (x1 == 0.0) x1 = T->mdct_zero_neg[1023 - 2 * q] ? -0.0 : 0.0;
+        X[2 * q] = x0;
+        X[1023 - 2 * q] = x1;
+    }
+    wave_sync();
+}
+
+// |FFT(d)[k]|, k < 1024, of a real 2048-sample block d(i) via a 1024-point
+// complex FFT.  buf: 1024 double2 of LDS; on return buf[k].x = |X[k]|.
+template <class DS>
+__device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
+                                                  double2* buf, int lane) {
+#pragma unroll 4
+    for (int n0 = 0; n0 < 1024; n0 += WAVE) {
+        int n = n0 + lane;
+        buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
+    }
+    wave_fft<10>(buf, T->fft_tw, lane);
+    // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k])
+#pragma unroll
+    for (int t0 = 0; t0 <= 512; t0 += WAVE) {
+        int k = t0 + lane;
+        if (k > 512) continue;
+        int k2 = (1024 - k) & 1023;
+        double2 Za = buf[k], Zb = buf[k2];
+        double mags[2];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            int kk = side ? k2 : k;
+            double2 A = side ? Zb : Za;   // Z[kk]
+            double2 Bc = side ? Za : Zb;  // Z[M-kk]
+            double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
+            double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
+            // -i * W^kk * o
+            double2 wo = cmul(T->rfft_tw[kk], o);
+            double xr = e.x + wo.y;
+            double xi = e.y - wo.x;
+            mags[side] = hypot(xr, xi);
+        }
+        buf[k].x = mags[0];
+        if (k2 != k) buf[k2].x = mags[1];
+    }
+    wave_sync();
+}
+
+struct Masker {
+    double z;    // Bark(f_m)
+    double B;    // (SPL_m - drop - 96) * log2(10)/10
+    double ku;   // (0.367*max(SPL_m-40,0) - 27) * log2(10)/10, upper slope (dz >= 0)
+};
+
+#define PAC_LOG2_10_OVER_10 0.33219280948873624   // log2(10)/10
+#define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
+
+// findpeaks (psychoac.py:158-191) on |X| held in buf[k].x, masker SPL from the
+// 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
+// compacted masker list (ascending frequency, the reference's summation order)
+// written over buf.  Returns the masker count.
+__device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
+                                                 double drop, int lane) {
+    const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
+    double S[16];
+    unsigned long long bal[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        int k = j * WAVE + lane;
+        bool pk = false;
+        S[j] = 0.0;
+        if (k >= 1 && k <= 1022) {
+            double m = buf[k].x;
+            pk = m > buf[k - 1].x && m > buf[k + 1].x && 10.0 * log10(m) > -30.0;
+        }
+        if (pk) {
+            double s = 0.0;
+            if (k >= 3) {
+                int hi = k + 3 < 1024 ? k + 3 : 1024;
+                for (int i = k - 3; i < hi; ++i) { double v = buf[i].x; s = __dadd_rn(s, __dmul_rn(v, v)); }
+            }
+            S[j] = pac_spl(csp * s);
+        }
+        bal[j] = __ballot(pk);
+    }
+    wave_sync();   // all magnitude reads done before the list overwrites buf
+    Masker* ml = reinterpret_cast<Masker*>(buf);
+    int base = 0;
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if ((bal[j] >> lane) & 1ull) {
+            int idx = base + __popcll(bal[j] & below);
+            int k = j * WAVE + lane;
+            double sp = S[j];
+            double lev = sp - 40.0;
+            lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
+            Masker mk;
+            mk.z = T->bark_bin[k];
+            mk.B = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
+            mk.ku = (lev - 27.0) * PAC_LOG2_10_OVER_10;
+            ml[idx] = mk;
+        }
+        base += __popcll(bal[j]);
+    }
+    wave_sync();
+    return base;
+}
+
+// Masking threshold (psychoac.py:447-456): for each MDCT line
+//   I(l) = sum_m 10^((spl_m(l) - 96)/10)  (ascending m, from 0.0)
+//   thr(l) = SPL(I(l) + Intensity(Thresh(f_l)))
+// with spl_m(l) = SPL_m + spread(dz) - drop written as the base-2 exponent
+// B_m + max(|dz| - 1/2, 0) * slope.  Lane owns lines l = 64 j + lane; the 16
+// rows are swept GRP at a time so the exp2 chains fit the register budget.
+template <int GRP = 4>
+__device__ __forceinline__ void wave_masking(const Masker* ml, int nm, const PacTables* __restrict__ T,
+                                             int lane, double thr[16]) {
+#pragma unroll
+    for (int j0 = 0; j0 < 16; j0 += GRP) {
+        double zl[GRP], acc[GRP];
+#pragma unroll
+        for (int j = 0; j < GRP; ++j) { zl[j] = T->bark_line[(j0 + j) * WAVE + lane]; acc[j] = 0.0; }
+#pragma unroll 1
+        for (int m = 0; m < nm; ++m) {
+            const double zm = ml[m].z, B = ml[m].B, ku = ml[m].ku;
+#pragma unroll
+            for (int j = 0; j < GRP; ++j) {
+                double dz = zl[j] - zm;
+                double a = fmax(fabs(dz) - 0.5, 0.0);
+                double k = dz >= 0.0 ? ku : PAC_KL;
+                acc[j] += pac_exp2(__builtin_fma(a, k, B));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GRP; ++j)
+            thr[j0 + j] = pac_spl(acc[j] + T->tiq[(j0 + j) * WAVE + lane]);
+    }
+}

@@ -1,0 +1,135 @@
+"""PAC/WAK coded-file plugin -- mirror of the reference's pacfile.py:115-383.
+
+``PACFile`` keeps the reference surface (ReadFileHeader / WriteFileHeader /
+WriteDataBlock / Close / Encode) and file layout:
+
+    'PAC ' <LHLLHH sampleRate nChannels numSamples nMDCTLines nScaleBits
+    nMantSizeBits> <L nBands> <nBands H nLines>   then per block, per channel:
+    <L nBytes> + nBytes of MSB-first packed bits.
+
+Every block is encoded by the HIP kernels (``codec.Encode`` ->
+``pac_encode_block``).  For throughput use the batch entry points
+``encode_file`` / ``encode_streams`` which run whole streams in one GPU call
+(``pac_encode_streams``); the bytes are identical.
+"""
+import struct
+
+import numpy as np
+
+from . import _lib
+from . import codec
+from .audiofile import AudioFile, CodingParams
+from .pcmfile import read_for_encode
+from .psychoac import AssignMDCTLinesFromFreqLimits, ScaleFactorBands
+
+PROFILE_ORIGIN = 0
+PROFILE_MASTER = 1
+
+
+def header_bytes(sampleRate, nChannels, numSamples, nMDCTLines=1024, nScaleBits=4,
+                 nMantSizeBits=4):
+    """File header as PACFile.WriteFileHeader writes it (pacfile.py:231-262),
+    including the inverted zero-padding quirk (pacfile.py:240-242): only an
+    exact multiple of nMDCTLines is bumped by one half-block."""
+    ns = numSamples
+    if not ns % nMDCTLines:
+        ns += nMDCTLines - ns % nMDCTLines
+    nLines = AssignMDCTLinesFromFreqLimits(nMDCTLines, sampleRate)
+    h = b"PAC " + struct.pack("<LHLLHH", sampleRate, nChannels, ns, nMDCTLines, nScaleBits,
+                              nMantSizeBits)
+    h += struct.pack("<L", len(nLines)) + struct.pack("<%dH" % len(nLines), *nLines)
+    return h
+
+
+class PACFile(AudioFile):
+    """Handlers for a perceptually coded audio file I am encoding/decoding."""
+
+    tag = b"PAC "
+
+    def __init__(self, filename, profile=PROFILE_MASTER, context=None):
+        super().__init__(filename)
+        self.profile = profile
+        self.context = context
+
+    def ReadFileHeader(self):
+        tag = self.fp.read(4)
+        if tag != self.tag:
+            raise ValueError("Tried to read a non-PAC file into a PACFile object")
+        (sampleRate, nChannels, numSamples, nMDCTLines, nScaleBits,
+         nMantSizeBits) = struct.unpack("<LHLLHH", self.fp.read(struct.calcsize("<LHLLHH")))
+        nBands = struct.unpack("<L", self.fp.read(4))[0]
+        nLines = struct.unpack("<%dH" % nBands, self.fp.read(2 * nBands))
+        p = CodingParams()
+        p.sampleRate = sampleRate
+        p.nChannels = nChannels
+        p.numSamples = numSamples
+        p.nMDCTLines = p.nSamplesPerBlock = nMDCTLines
+        p.nScaleBits = nScaleBits
+        p.nMantSizeBits = nMantSizeBits
+        p.sfBands = ScaleFactorBands(nLines)
+        p.overlapAndAdd = [np.zeros(nMDCTLines, dtype=np.float64) for _ in range(nChannels)]
+        return p
+
+    def ReadDataBlock(self, codingParams, huffman=None):
+        raise NotImplementedError("decoder path is the next row of SURVEY.md 8(f)")
+
+    def WriteFileHeader(self, codingParams):
+        self.fp.write(header_bytes(codingParams.sampleRate, codingParams.nChannels,
+                                   codingParams.numSamples, codingParams.nMDCTLines,
+                                   codingParams.nScaleBits, codingParams.nMantSizeBits))
+        if not codingParams.numSamples % codingParams.nMDCTLines:
+            codingParams.numSamples += (codingParams.nMDCTLines
+                                        - codingParams.numSamples % codingParams.nMDCTLines)
+        codingParams.sfBands = ScaleFactorBands(
+            AssignMDCTLinesFromFreqLimits(codingParams.nMDCTLines, codingParams.sampleRate))
+        codingParams.priorBlock = [np.zeros(codingParams.nMDCTLines, dtype=np.float64)
+                                   for _ in range(codingParams.nChannels)]
+        codingParams.extraBits = 0
+        codingParams.curBlock = 0
+
+    def WriteDataBlock(self, data, codingParams, huffman=None):
+        full = [np.concatenate((codingParams.priorBlock[c], data[c]))
+                for c in range(codingParams.nChannels)]
+        codingParams.priorBlock = data
+        raw = codec.encode_block_bytes(full, codingParams, huffman, self.profile, self.context)
+        self.fp.write(raw)
+
+    def Close(self, codingParams, huffman=None):
+        if self.fp.mode == "wb":
+            data = [np.zeros(codingParams.nMDCTLines) for _ in range(codingParams.nChannels)]
+            self.WriteDataBlock(data, codingParams, huffman)
+        self.fp.close()
+
+    def Encode(self, data, codingParams, huffman=None):
+        return codec.Encode(data, codingParams, huffman, profile=self.profile,
+                            context=self.context)
+
+
+# ---------------------------------------------------------------------------
+# batch entry points (one GPU call for whole streams)
+# ---------------------------------------------------------------------------
+
+def encode_streams(streams, sample_rate, profile=PROFILE_MASTER, context=None, states=None):
+    """Encode independent streams (list of int16 [frames, nCh] arrays sharing
+    sample rate and channel count).  Returns a list of data-section bytes."""
+    ctx = context or codec.default_context()
+    nch = streams[0].shape[1]
+    fo = np.zeros(len(streams) + 1, dtype=np.int64)
+    fo[1:] = np.cumsum([s.shape[0] for s in streams])
+    pcm = np.concatenate([np.ascontiguousarray(s, dtype=np.int16) for s in streams]) \
+        if len(streams) > 1 else np.ascontiguousarray(streams[0], dtype=np.int16)
+    p = _lib.params(sample_rate, nch, profile)
+    out, so = ctx.encode_streams(p, pcm, fo, states=states)
+    return [out[so[i]:so[i + 1]].tobytes() for i in range(len(streams))]
+
+
+def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):
+    """The reference driver's encode half (pacfile.py:430-499) for one file,
+    as a single GPU call.  Returns the coded file bytes (and writes them)."""
+    cp, frames = read_for_encode(in_path)
+    body = encode_streams([frames], cp.sampleRate, profile, context)[0]
+    data = header_bytes(cp.sampleRate, cp.nChannels, cp.numSamples) + body
+    if out_path:
+        with open(out_path, "wb") as f:
+            f.write(data)
+    return data

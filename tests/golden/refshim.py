@@ -134,6 +134,8 @@ def edit(mod, src, profile):
                      HUFF_INIT, src, count=1, flags=re.S)
         assert "PACHUF01" in src
         src = _sub(src, "extraBit = self.bitDeposit/100", "extraBit = self.bitDeposit//100")
+    if mod == "bitalloc":
+        src = src.replace("print('*')", "pass")
     if mod == "codec" and profile == "master":
         src = _sub(src, "sum(len(huff) for huff in m)", "__import__('builtins').sum(len(huff) for huff in m)")
     return src

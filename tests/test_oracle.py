@@ -1,0 +1,162 @@
+"""The CPU oracle (oracle/pac_oracle.c) pinned against the reference's own
+outputs: committed fixture bitstreams and the per-stage golden vectors that
+tests/golden/make_golden.py dumped from the reference code.  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, REF, fixture
+
+import pyoracle as P
+from pac_amd.pcmfile import codes_to_float
+
+GOLDEN_CASES = ["origin_white48k", "origin_zero48k", "origin_square44k", "origin_mono44k",
+                "master_pinktones48k", "master_zero48k", "master_square44k", "master_white48k"]
+
+
+def golden_case(name):
+    pcm = np.load(os.path.join(GOLD, name + ".in.npy"))
+    ext = "pac" if name.startswith("origin") else "wak"
+    with open(os.path.join(GOLD, "%s.%s" % (name, ext)), "rb") as f:
+        coded = f.read()
+    st = dict(np.load(os.path.join(GOLD, "stages_%s.npz" % name)))
+    return pcm, coded, st
+
+
+def oracle_file(pcm, fs, profile):
+    o = P.Oracle(fs, huffman=(profile == P.MASTER))
+    return P.pac_header(fs, pcm.shape[1], pcm.shape[0], o.nlines()) + o.encode_data(profile, pcm)
+
+
+def test_harpsichord_pac_fixture():
+    assert P.encode_file(fixture("harpsichord.wav"), P.ORIGIN) == open(fixture("harpsichord.pac"), "rb").read()
+
+
+def test_piano_test2_wak_fixture():
+    assert P.encode_file(fixture("piano_test2.wav"), P.MASTER) == open(fixture("piano_test2.wak"), "rb").read()
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_golden_bitstreams(name):
+    pcm, coded, st = golden_case(name)
+    fs = int(st["fs"])
+    prof = P.ORIGIN if name.startswith("origin") else P.MASTER
+    assert oracle_file(pcm, fs, prof) == coded
+
+
+def _blocks(pcm):
+    """float64 full blocks (priorBlock ++ hop) per block index, per channel."""
+    x = codes_to_float(pcm.astype(np.int64))
+    n, nch = x.shape
+    hops = (n + 1023) // 1024
+    padded = np.zeros(((hops + 1) * 1024, nch))
+    padded[:n] = x
+    prior = np.zeros((1024, nch))
+
+    def blk(b):
+        lo = (b - 1) * 1024
+        pre = prior if b == 0 else padded[lo:lo + 1024]
+        cur = padded[b * 1024:(b + 1) * 1024]
+        return np.concatenate([pre, cur]).T
+    return blk
+
+
+@pytest.mark.parametrize("name", [c for c in GOLDEN_CASES if c.startswith("origin")])
+def test_origin_stages(name):
+    """Per-stage parity with the reference on selected blocks: MDCT (1e-9 rel to
+    the block max), threshold (1e-9 dB), SMR (1e-9 dB), exact ints."""
+    pcm, coded, st = golden_case(name)
+    fs = int(st["fs"])
+    o = P.Oracle(fs, huffman=False)
+    blk = _blocks(pcm)
+    nch = pcm.shape[1]
+    for i, b in enumerate(st["ba_block"]):
+        c = i % nch
+        ob = o.block_origin(blk(int(b))[c])
+        ref_mdct = st["mdct"][i]
+        scale = max(np.max(np.abs(ref_mdct)), 1e-300)
+        assert np.max(np.abs(np.array(ob.mdct[:]) - ref_mdct)) <= 1e-9 * scale
+        assert np.array_equal(np.signbit(np.array(ob.mdct[:])), np.signbit(ref_mdct)) or scale > 1e-300
+        assert np.max(np.abs(np.array(ob.thr[:]) - st["thr"][i])) < 1e-9
+        assert np.max(np.abs(np.array(ob.smr[:]) - st["smr"][i])) < 1e-9
+        assert list(ob.ba) == list(st["ba"][i].astype(int))
+        assert list(ob.sf) == list(st["sf"][i].astype(int))
+        assert ob.overall == int(st["overall"][i])
+
+
+@pytest.mark.parametrize("name", [c for c in GOLDEN_CASES if c.startswith("master")])
+def test_master_stages(name):
+    pcm, coded, st = golden_case(name)
+    fs = int(st["fs"])
+    o = P.Oracle(fs, huffman=True)
+    blk = _blocks(pcm)
+    state = P.State()
+    want = set(int(b) for b in st["ba_block"])
+    nb = max(want) + 1
+    k = 0
+    for b in range(nb):
+        x = blk(b)
+        ob = o.block_master(x[0], x[1], state)
+        if b not in want:
+            continue
+        assert list(ob.lrms) == list(st["lrms"][k].astype(int))
+        for c in range(2):
+            assert list(ob.ba[c]) == list(st["ba"][k][c].astype(int))
+            assert list(ob.sf[c]) == list(st["sf"][k][c].astype(int))
+            assert ob.overall[c] == int(st["overall"][k][c])
+            assert np.max(np.abs(np.array(ob.smr[c][:]) - st["smr"][k][c])) < 1e-9
+        for v in range(6):
+            assert np.max(np.abs(np.array(ob.bthr[v][:]) - st["thr"][6 * k + v])) < 1e-9
+        for c in range(2):
+            ref = st["mdct"][2 * k + c]
+            scale = max(np.max(np.abs(ref)), 1e-300)
+            assert np.max(np.abs(np.array(ob.mdct[c][:]) - ref)) <= 1e-9 * scale
+        k += 1
+
+
+def test_zero_block_mdct_signs_match_reference():
+    """An all-zero block's MDCT lines are signed zeros whose signs reach the
+    bitstream through vMantissa (quantize.py:333); the golden zero streams
+    pin them end to end.  Here: the oracle's signs equal the reference
+    post-twiddle rule Re(+0 * tw) = (+0*cos) - (+0*sin) (mdct.py:355)."""
+    o = P.Oracle(48000, huffman=False)
+    X = o.mdct(np.zeros(2048))
+    assert np.all(X == 0)
+    k = np.arange(1024)
+    tw = np.exp(1j * (-2. * np.pi / 2048) * 512.5 * (k + (1 / 2.)))
+    neg = (tw.real < 0) & (tw.imag >= 0)
+    assert np.array_equal(np.signbit(X), neg)
+
+
+REF_FIXTURES = [("inputs/harpsichord.wav", "coded/harpsichord.pac", P.ORIGIN),
+                ("PerceptualAudioCodec_Origin/inputs/german.wav", "coded/german.pac", P.ORIGIN),
+                ("PerceptualAudioCodec_Origin/inputs/trumpet.wav", "coded/trumpet.pac", P.ORIGIN)] + [
+    ("inputs/%s.wav" % n, "coded/%s.wak" % n, P.MASTER) for n in
+    ("piano_test2 harmonic_test2 harmonic_test4 percussion_test1 percussion_test2 "
+     "percussion_test3 piano_test3 pop_test2 rock rock_test2 speech_test2 speech_test3").split()] + [
+    ("inputs/speech_test3.wav", "coded/withHuffman/speech_test3.wak", P.MASTER)]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+@pytest.mark.parametrize("inp,coded,prof", REF_FIXTURES, ids=[c for _, c, _ in REF_FIXTURES])
+def test_reference_fixture_prefix(inp, coded, prof):
+    """Every verified reference bitstream: the first 48
+    blocks byte for byte (the encoder is causal, so a prefix is a full check
+    of those blocks incl. the reservoir chain)."""
+    fs, nch, n, pcm = P.read_wav(os.path.join(REF, inp))
+    o = P.Oracle(fs, huffman=(prof == P.MASTER))
+    got = P.pac_header(fs, nch, n, o.nlines()) + o.encode_data(prof, pcm, max_blocks=48)
+    with open(os.path.join(REF, coded), "rb") as f:
+        ref = f.read()
+    assert got == ref[:len(got)]
+
+
+def test_manifest_hashes():
+    with open(os.path.join(GOLD, "manifest.json")) as f:
+        m = json.load(f)
+    import hashlib
+    for fn, h in m["files"].items():
+        with open(os.path.join(GOLD, fn), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == h, fn

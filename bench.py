@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo 1024-sample blocks encoded per second on MI355X.
+
+Workload (BASELINE.json configs[1], the config the metric is quoted on):
+synthetic 48 kHz stereo white noise, N(0,1)*0.25*32767 rounded/clipped to
+int16, 10^6 stereo blocks per GPU (1000 independent streams x 1000 blocks,
+999 hops + the Close() flush block each), origin profile ("M/S off":
+PerceptualAudioCodec_Origin's coder, the reference's own no-M/S encoder).
+The PCM is generated on the device (k_synth_white) so the timed region starts
+with the inputs resident in HBM; one step = one pac_encode_streams call over
+all 10^6 blocks (MDCT, masking threshold, bit allocation, quantization, bit
+packing into the .pac data sections, all in HBM).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Streams shard across ranks with no data-path collective (weak scaling); the
+only cross-rank traffic is the barrier and the max-over-ranks of the timer
+(gloo, CPU tensors).  Rank 0 prints one JSON line.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import pac_amd  # noqa: E402,F401
+from pac_amd import _lib  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=1000)
+    ap.add_argument("--blocks-per-stream", type=int, default=1000)
+    ap.add_argument("--sample-rate", type=int, default=48000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="bounded CPU-baseline sample (oracle on host cores)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+class Dist:
+    """Barrier + max over ranks; gloo on CPU when launched under torchrun."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.td = None
+        if self.world > 1:
+            import torch.distributed as td
+            td.init_process_group("gloo")
+            self.td = td
+
+    def barrier(self):
+        if self.td:
+            self.td.barrier()
+
+    def max(self, v):
+        if not self.td:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if not self.td:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.td:
+            self.td.destroy_process_group()
+
+
+def cpu_baseline(ctx, dev_pcm, frames_per_stream, fs, seconds):
+    """The CPU oracle (oracle/pac_oracle.c, 1 thread) on a bounded sample of
+    the same workload: the first hops of stream 0, copied back from HBM."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as P
+    P.lib()
+    hops = min(frames_per_stream // 1024, 4096)
+    pcm = np.empty((hops * 1024, 2), dtype=np.int16)
+    ctx.to_host(pcm, dev_pcm)
+    o = P.Oracle(fs, huffman=False)
+    done, t0, chunk = 0, time.perf_counter(), 16
+    while True:
+        n = min(chunk, hops - 1)
+        o.encode_data(P.ORIGIN, pcm[: n * 1024], max_blocks=n)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= 200000:
+            break
+        chunk = min(chunk * 2, hops - 1)
+    return {"value": done / el, "unit": "blocks/s", "cores": 1, "kind": "port",
+            "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
+                      "fixtures), 1 host thread, %d stereo blocks of the same synthetic "
+                      "48 kHz white-noise stream in %.1f s" % (done, el)}
+
+
+def main():
+    a = parse()
+    dist = Dist()
+    ctx = _lib.Context(dist.local, huffman=False)
+    fs = a.sample_rate
+    hops = a.blocks_per_stream - 1
+    fps = hops * 1024
+    ns = a.streams
+    n_frames = ns * fps
+    fo = np.arange(ns + 1, dtype=np.int64) * fps
+    p = _lib.params(fs, 2, 0)
+    blocks = ns * a.blocks_per_stream
+    pcm_dev = ctx.alloc(n_frames * 2 * 2)
+    ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * dist.rank)
+    cap = int(ctx.L.pac_encode_bound(C.byref(p), ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
+    out_dev = ctx.alloc(cap)
+    ctx.set_timing(True)
+
+    def step():
+        return ctx.encode_streams(p, pcm_dev, fo, out=out_dev, out_capacity=cap,
+                                  pcm_is_device=True, out_is_device=True)
+
+    for _ in range(a.warmup):
+        step()
+    fronts, alloc_ms, pack_ms, totals = [], [], [], []
+    dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _, so = step()
+        t = ctx.last_timing()
+        fronts.append(t.front_ms)
+        alloc_ms.append(t.alloc_ms)
+        pack_ms.append(t.pack_ms)
+        totals.append(t.total_ms)
+    ctx.sync()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    el_max = dist.max(el)
+    out_bytes = int(so[-1])
+    total_blocks = dist.sum(blocks)
+    value = total_blocks / (el_max / a.steps)
+
+    # roofline of the dominant kernel (k_origin_front): algorithmic bytes per
+    # launch = int16 PCM read (4096 B per stereo block) + SMR/peak/scale
+    # outputs (2 x (25*8 + 25*8 + 1) B per stereo block)
+    front_s = float(np.mean(fronts)) / 1e3
+    alg_bytes = blocks * (4096 + 2 * (25 * 8 * 2 + 1))
+    achieved = alg_bytes / front_s / 1e9
+    # FP64 work of the masking sum: ~20 fp64 VALU ops per masker-line pair is
+    # measured by PMC (profiles/); here only report the pair count per block
+    res = {
+        "metric": "stereo 1024-sample blocks encoded/s",
+        "value": value,
+        "unit": "blocks/s",
+        "n_gpus": dist.world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": el_max / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (device-generated white noise, counter-hash Box-Muller)",
+        "config": {"workload": "BASELINE configs[1]: synthetic 48 kHz stereo white noise, "
+                               "10^6 stereo blocks per GPU, N=1024 MDCT, M/S off "
+                               "(origin profile)",
+                   "profile": "origin", "sample_rate": fs, "streams_per_gpu": ns,
+                   "blocks_per_stream": a.blocks_per_stream,
+                   "global_blocks": int(total_blocks), "parallelism": "streams sharded, %d rank(s)"
+                   % dist.world},
+        "roofline": {"bound": "hbm", "kernel": "k_origin_front", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None,
+                     "note": "path is FP64-VALU bound (masking sum), see DESIGN.md"},
+        "kernels_ms": {"front": float(np.mean(fronts)), "alloc": float(np.mean(alloc_ms)),
+                       "pack": float(np.mean(pack_ms)), "step_device": float(np.mean(totals))},
+        "out_bytes_per_gpu": out_bytes,
+    }
+    if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(ctx, pcm_dev, fps, fs, a.cpu_seconds)
+    ctx.free(out_dev)
+    ctx.free(pcm_dev)
+    if dist.rank == 0:
+        print(json.dumps(res))
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

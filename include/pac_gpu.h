@@ -129,6 +129,8 @@ int pac_copy_to_host(pac_ctx *ctx, void *dst, const void *src, int64_t bytes);
 int pac_synth_white(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_samples, uint64_t seed);
 int pac_sync(pac_ctx *ctx);
 int pac_set_timing(pac_ctx *ctx, int32_t enable);
+/* Stereo blocks per master-profile chunk (device scratch ~65 KB/block). */
+int pac_set_chunk_blocks(pac_ctx *ctx, int64_t blocks);
 int pac_last_timing(pac_ctx *ctx, pac_timing *out);
 
 #ifdef __cplusplus

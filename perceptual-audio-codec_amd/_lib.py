@@ -85,6 +85,7 @@ def lib():
         "pac_synth_white": (C.c_int, [vp, vp, i64, C.c_uint64]),
         "pac_sync": (C.c_int, [vp]),
         "pac_set_timing": (C.c_int, [vp, i32]),
+        "pac_set_chunk_blocks": (C.c_int, [vp, i64]),
         "pac_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
     }
     for name, (res, args) in sig.items():

@@ -11,11 +11,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/pac_gpu.h"
 #include "pac_kernels.hip"
+#include "pac_master.hip"
 
 #define PAC_VERSION 100
 
@@ -181,6 +184,13 @@ struct pac_ctx {
     DevBuf<int16_t> pcm_stage;
     DevBuf<uint8_t> out_stage;
     DevBuf<double> fsrc;
+    // master
+    DevBuf<double> m_thr, m_lines, m_smr, m_peak;
+    DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
+    DevBuf<int64_t> st_extra, st_deposit, base;
+    PacHuffTables* huff_host = nullptr;
+    std::unordered_map<uint64_t, int> huff_dec[PAC_NTAB];   // (len<<32|code) -> symbol, -1 = escape
+    int64_t chunk_blocks = 32768;
     // timing
     bool timing = false;
     hipEvent_t ev[5] = {};
@@ -210,6 +220,10 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (auto& kv : c->tables) hipFree(kv.second);
     if (c->huff) hipFree(c->huff);
+    free(c->huff_host);
+    c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
+    c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
+    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->base.release();
     c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
@@ -284,7 +298,14 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
         return set_err(PAC_E_NOMEM, "device huffman tables");
     }
     hipError_t e = hipMemcpy(c->huff, h, sizeof(PacHuffTables), hipMemcpyHostToDevice);
-    free(h);
+    free(c->huff_host);
+    c->huff_host = h;    // kept for pac_encode_block's field reconstruction
+    for (int t = 0; t < PAC_NTAB; t++) {
+        c->huff_dec[t].clear();
+        for (int sym = 0; sym < PAC_NSYM; sym++)
+            if (h->len[t][sym]) c->huff_dec[t][((uint64_t)h->len[t][sym] << 32) | h->bits[t][sym]] = sym;
+        c->huff_dec[t][((uint64_t)h->esc_len[t] << 32) | h->esc_bits[t]] = -1;
+    }
     if (e != hipSuccess) return set_err(PAC_E_HIP, "huffman upload: %s", hipGetErrorString(e));
     c->have_huff = true;
     return PAC_OK;
@@ -386,20 +407,112 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     c->last.out_bytes = bytes;
 }
 
+// --- master: chunks of whole-block ranges, stream-major ----------------------
+
+// Runs the master pipeline over global blocks [0, nblocks).  States (device
+// st_extra / st_deposit, per stream) must be initialised by the caller.
+static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src,
+                      const std::vector<int64_t>& blk, uint8_t* out_dev, int64_t out_cap,
+                      int64_t* out_total) {
+    int rc;
+    const int n_streams = src.n_streams;
+    const int64_t nblocks = blk[n_streams];
+    const int64_t CB = c->chunk_blocks;
+    const int64_t cb = nblocks < CB ? nblocks : CB;
+    if ((rc = c->m_thr.ensure(cb * 6 * PAC_HALFN)) || (rc = c->m_lines.ensure(cb * 2 * PAC_HALFN)) ||
+        (rc = c->m_smr.ensure(cb * 2 * PAC_NB)) || (rc = c->m_peak.ensure(cb * 2 * PAC_NB)) ||
+        (rc = c->m_lrms.ensure(cb * PAC_NB)) || (rc = c->m_overall.ensure(cb * 2)) ||
+        (rc = c->m_ba.ensure(cb * 2 * PAC_NB)) || (rc = c->m_sf.ensure(cb * 2 * PAC_NB)) ||
+        (rc = c->m_tid.ensure(cb * 2)) || (rc = c->nbytes.ensure(cb * 2)) ||
+        (rc = c->off.ensure(cb * 2 + 1)) ||
+        (rc = c->tile_sums.ensure((cb * 2 + SCAN_TILE - 1) / SCAN_TILE + 1)) ||
+        (rc = c->grand_total.ensure(1)) || (rc = c->base.ensure(1)))
+        return rc;
+    PacMasterWork W{c->m_thr.p, c->m_lines.p, c->m_smr.p, c->m_peak.p, c->m_lrms.p, c->m_overall.p,
+                    c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p};
+    hipStream_t s = c->stream;
+    const double budget = bit_budget(p);
+    HIPCHK(hipMemsetAsync(c->base.p, 0, sizeof(int64_t), s));
+    float t_front = 0, t_alloc = 0, t_scan = 0, t_pack = 0;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
+    for (int64_t gb0 = 0; gb0 < nblocks; gb0 += CB) {
+        const int64_t gb1 = gb0 + CB < nblocks ? gb0 + CB : nblocks;
+        const int64_t B = gb1 - gb0, G = 2 * B;
+        int s_first = (int)(std::upper_bound(blk.begin(), blk.end(), gb0) - blk.begin()) - 1;
+        int s_last = (int)(std::upper_bound(blk.begin(), blk.end(), gb1 - 1) - blk.begin()) - 1;
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(64), 0, s, src, T, W, gb0);
+        hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(64), 0, s, src, T, W, gb0);
+        HIPCHK(hipGetLastError());
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
+        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)(s_last - s_first + 1)), dim3(64), 0, s, T, c->huff,
+                           W, c->blk_off.p, s_first, gb0, gb1, c->st_extra.p, c->st_deposit.p, budget);
+        HIPCHK(hipGetLastError());
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
+        int64_t ntiles = (G + SCAN_TILE - 1) / SCAN_TILE;
+        hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G, c->tile_sums.p);
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tile_sums.p, ntiles, c->grand_total.p);
+        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G,
+                           c->tile_sums.p, c->off.p);
+        int64_t base = 0, tot = 0;
+        HIPCHK(hipMemcpyAsync(&base, c->base.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&tot, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (base + tot > out_cap)
+            return set_err(PAC_E_CAPACITY, "output needs > %lld bytes, capacity %lld",
+                           (long long)(base + tot), (long long)out_cap);
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[4], s));
+        hipLaunchKernelGGL(k_master_pack, dim3((unsigned)G), dim3(64), 0, s, T, c->huff, W, c->off.p,
+                           c->base.p, out_dev);
+        hipLaunchKernelGGL(k_master_stream_offsets, dim3((n_streams + 255) / 256), dim3(256), 0, s, c->off.p,
+                           c->blk_off.p, n_streams, gb0, gb1, c->base.p, c->stream_off.p);
+        hipLaunchKernelGGL(k_add_base, dim3(1), dim3(64), 0, s, c->base.p, c->grand_total.p);
+        HIPCHK(hipGetLastError());
+        if (c->timing) {
+            HIPCHK(hipEventRecord(c->ev[0], s));   // reuse as chunk end
+            HIPCHK(hipEventSynchronize(c->ev[0]));
+            float a, b2, c3, d;
+            hipEventElapsedTime(&a, c->ev[1], c->ev[2]);
+            hipEventElapsedTime(&b2, c->ev[2], c->ev[3]);
+            hipEventElapsedTime(&c3, c->ev[3], c->ev[4]);
+            hipEventElapsedTime(&d, c->ev[4], c->ev[0]);
+            t_front += a; t_alloc += b2; t_scan += c3; t_pack += d;
+        }
+    }
+    int64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, c->base.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (c->timing) {
+        c->last.front_ms = t_front;
+        c->last.alloc_ms = t_alloc;
+        c->last.scan_ms = t_scan;
+        c->last.pack_ms = t_pack;
+        c->last.total_ms = t_front + t_alloc + t_scan + t_pack;
+        c->last.n_channel_blocks = 2 * nblocks;
+        c->last.out_bytes = total;
+    }
+    *out_total = total;
+    return PAC_OK;
+}
+
+__global__ void k_set_last(int64_t* __restrict__ so, int n, const int64_t* __restrict__ base) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) so[n] = *base;
+}
+
 extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_streams, const int16_t* pcm,
                                   const int64_t* frame_offsets, int32_t pcm_is_device, uint8_t* out,
                                   int64_t out_capacity, int32_t out_is_device, int64_t* stream_byte_offsets,
                                   pac_stream_state* states) {
-    (void)states;
     int rc;
     if (!c || !frame_offsets || !out || !stream_byte_offsets || n_streams < 1)
         return set_err(PAC_E_ARG, "null argument or n_streams < 1");
     if ((rc = check_params(p))) return rc;
-    if (p->profile != PAC_PROFILE_ORIGIN)
-        return set_err(PAC_E_UNSUPPORTED, "master profile: pac_encode_streams not built yet");
+    const bool master = p->profile == PAC_PROFILE_MASTER;
+    if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
+    if (frame_offsets[0] != 0) return set_err(PAC_E_ARG, "frame_offsets[0] must be 0");
     for (int s = 0; s < n_streams; s++)
-        if (frame_offsets[s + 1] < frame_offsets[s] || frame_offsets[0] != 0)
-            return set_err(PAC_E_ARG, "frame_offsets must start at 0 and be non-decreasing");
+        if (frame_offsets[s + 1] < frame_offsets[s])
+            return set_err(PAC_E_ARG, "frame_offsets must be non-decreasing");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
     if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
@@ -435,16 +548,34 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     }
     PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch};
     int64_t total = 0;
-    int64_t* off_dev = nullptr;
-    if ((rc = run_origin(c, p, T, src, G, out_dev, out_capacity, &total, &off_dev))) return rc;
-    hipLaunchKernelGGL(k_stream_offsets, dim3((n_streams + 1 + 255) / 256), dim3(256), 0, s, off_dev,
-                       c->blk_off.p, n_streams, nch, c->grand_total.p, c->stream_off.p);
-    HIPCHK(hipGetLastError());
+    if (master) {
+        if ((rc = c->st_extra.ensure(n_streams)) || (rc = c->st_deposit.ensure(n_streams))) return rc;
+        std::vector<int64_t> ex(n_streams, 0), dp(n_streams, 0);
+        if (states)
+            for (int i = 0; i < n_streams; i++) { ex[i] = states[i].extra_bits; dp[i] = states[i].bit_deposit; }
+        HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total))) return rc;
+        hipLaunchKernelGGL(k_set_last, dim3(1), dim3(64), 0, s, c->stream_off.p, n_streams, c->base.p);
+        HIPCHK(hipGetLastError());
+        if (states) {
+            HIPCHK(hipMemcpyAsync(ex.data(), c->st_extra.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(dp.data(), c->st_deposit.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (int i = 0; i < n_streams; i++) { states[i].extra_bits = ex[i]; states[i].bit_deposit = dp[i]; }
+        }
+    } else {
+        int64_t* off_dev = nullptr;
+        if ((rc = run_origin(c, p, T, src, G, out_dev, out_capacity, &total, &off_dev))) return rc;
+        hipLaunchKernelGGL(k_stream_offsets, dim3((n_streams + 1 + 255) / 256), dim3(256), 0, s, off_dev,
+                           c->blk_off.p, n_streams, nch, c->grand_total.p, c->stream_off.p);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipMemcpyAsync(stream_byte_offsets, c->stream_off.p, (n_streams + 1) * sizeof(int64_t),
                           hipMemcpyDeviceToHost, s));
     if (!out_is_device && total) HIPCHK(hipMemcpyAsync(out, out_dev, total, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    finish_timing(c, G, total);
+    if (!master) finish_timing(c, G, total);
     return PAC_OK;
 }
 
@@ -460,36 +591,71 @@ struct BitReader {
     }
 };
 
+// Huffman.decodeData (Huffman.py:321-344) on the host copy of the tables, used
+// only to hand the codec.Encode() tuple back to the plugin surface.
+static uint32_t host_huff_decode(const std::unordered_map<uint64_t, int>& dec, const PacHuffTables* h,
+                                 int tid, BitReader& br, int ba) {
+    uint32_t code = 0;
+    for (int len = 1; len <= 32; len++) {
+        code = (code << 1) | br.get(1);
+        auto it = dec.find(((uint64_t)len << 32) | code);
+        if (it != dec.end()) return it->second < 0 ? br.get(ba) : (uint32_t)it->second;
+    }
+    (void)h;
+    (void)tid;
+    return 0;
+}
+
 extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* full_block,
                                 pac_stream_state* state, uint8_t* out, int64_t out_capacity, int64_t* out_bytes,
                                 pac_block_fields* fields) {
-    (void)state;
     int rc;
     if (!c || !full_block || !out || !out_bytes) return set_err(PAC_E_ARG, "null argument");
     if ((rc = check_params(p))) return rc;
-    if (p->profile != PAC_PROFILE_ORIGIN)
-        return set_err(PAC_E_UNSUPPORTED, "master profile: pac_encode_block not built yet");
+    const bool master = p->profile == PAC_PROFILE_MASTER;
+    if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
     if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
     const int nch = p->n_channels;
     const int64_t G = nch;
     hipStream_t s = c->stream;
-    if ((rc = c->fsrc.ensure(G * PAC_N)) || (rc = c->out_stage.ensure(G * 4200))) return rc;
+    if ((rc = c->fsrc.ensure(G * PAC_N)) || (rc = c->out_stage.ensure(G * 8400)) ||
+        (rc = c->blk_off.ensure(2)) || (rc = c->stream_off.ensure(2)))
+        return rc;
     HIPCHK(hipMemcpyAsync(c->fsrc.p, full_block, G * PAC_N * sizeof(double), hipMemcpyHostToDevice, s));
-    PacSource src{nullptr, nullptr, nullptr, c->fsrc.p, 1, nch};
+    PacSource src{nullptr, nullptr, c->blk_off.p, c->fsrc.p, 1, nch};
     int64_t total = 0;
-    int64_t* off_dev = nullptr;
-    if ((rc = run_origin(c, p, T, src, G, c->out_stage.p, c->out_stage.n, &total, &off_dev))) return rc;
+    std::vector<double> smr(PAC_NB * G);
+    int32_t lrms[PAC_NB] = {0};
+    if (master) {
+        std::vector<int64_t> blk = {0, 1};
+        HIPCHK(hipMemcpyAsync(c->blk_off.p, blk.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if ((rc = c->st_extra.ensure(1)) || (rc = c->st_deposit.ensure(1))) return rc;
+        int64_t ex = state ? state->extra_bits : 0, dp = state ? state->bit_deposit : 0;
+        HIPCHK(hipMemcpyAsync(c->st_extra.p, &ex, sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->st_deposit.p, &dp, sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if ((rc = run_master(c, p, T, src, blk, c->out_stage.p, c->out_stage.n, &total))) return rc;
+        HIPCHK(hipMemcpyAsync(&ex, c->st_extra.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&dp, c->st_deposit.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(smr.data(), c->m_smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        uint8_t lr[PAC_NB];
+        HIPCHK(hipMemcpyAsync(lr, c->m_lrms.p, PAC_NB, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int b = 0; b < PAC_NB; b++) lrms[b] = lr[b];
+        if (state) { state->extra_bits = ex; state->bit_deposit = dp; }
+    } else {
+        int64_t* off_dev = nullptr;
+        if ((rc = run_origin(c, p, T, src, G, c->out_stage.p, c->out_stage.n, &total, &off_dev))) return rc;
+        HIPCHK(hipMemcpyAsync(smr.data(), c->smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        finish_timing(c, G, total);
+    }
     if (total > out_capacity) return set_err(PAC_E_CAPACITY, "block needs %lld bytes", (long long)total);
     HIPCHK(hipMemcpyAsync(out, c->out_stage.p, total, hipMemcpyDeviceToHost, s));
-    std::vector<double> smr(PAC_NB * G);
-    HIPCHK(hipMemcpyAsync(smr.data(), c->smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    finish_timing(c, G, total);
     *out_bytes = total;
     if (fields) {
-        // reconstruct the codec.Encode() tuple from the GPU-written channel-blocks
+        // the codec.Encode() tuple, read back from the GPU-written channel-blocks
         memset(fields, 0, sizeof(*fields));
         fields->n_channels = nch;
         int32_t nl[PAC_NB];
@@ -500,18 +666,30 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
             fields->nbytes[ch] = (int32_t)nb;
             BitReader br{out + o + 4, 0};
             fields->overall[ch] = (int32_t)br.get(4);
+            int tid = master ? (int)br.get(4) : 0;
+            fields->table_id[ch] = tid;
             int line = 0;
             for (int b = 0; b < PAC_NB; b++) {
                 int ba = (int)br.get(4);
                 if (ba) ba++;
                 fields->ba[ch][b] = ba;
                 fields->sf[ch][b] = (int32_t)br.get(4);
-                fields->smr[ch][b] = smr[b * G + ch];
-                for (int l = 0; l < nl[b]; l++) fields->mant[ch][line + l] = ba ? (int32_t)br.get(ba) : 0;
+                fields->smr[ch][b] = master ? smr[ch * PAC_NB + b] : smr[b * G + ch];
+                if (!master) {
+                    for (int l = 0; l < nl[b]; l++) fields->mant[ch][line + l] = ba ? (int32_t)br.get(ba) : 0;
+                } else if (ba) {
+                    uint32_t sg[1024];
+                    for (int l = 0; l < nl[b]; l++) sg[l] = br.get(1);
+                    for (int l = 0; l < nl[b]; l++) {
+                        uint32_t mag = host_huff_decode(c->huff_dec[tid - 1], c->huff_host, tid - 1, br, ba);
+                        fields->mant[ch][line + l] = (int32_t)(mag + (sg[l] << (ba - 1)));
+                    }
+                }
                 line += nl[b];
             }
             o += 4 + nb;
         }
+        for (int b = 0; b < PAC_NB; b++) fields->lrms[b] = lrms[b];
     }
     return PAC_OK;
 }
@@ -561,6 +739,11 @@ extern "C" int pac_sync(pac_ctx* c) {
 extern "C" int pac_set_timing(pac_ctx* c, int32_t enable) {
     if (!c) return set_err(PAC_E_ARG, "null ctx");
     c->timing = enable != 0;
+    return PAC_OK;
+}
+extern "C" int pac_set_chunk_blocks(pac_ctx* c, int64_t blocks) {
+    if (!c || blocks < 1) return set_err(PAC_E_ARG, "bad argument");
+    c->chunk_blocks = blocks;
     return PAC_OK;
 }
 extern "C" int pac_last_timing(pac_ctx* c, pac_timing* out) {

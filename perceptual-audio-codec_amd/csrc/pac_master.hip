@@ -1,0 +1,501 @@
+// pac_master.hip -- gfx950 kernels of the master (.wak) profile: codec/ of the
+// reference (M/S decision, six masking thresholds, bit reservoir, Huffman).
+//
+// Per chunk of Bc stereo blocks (whole-stream block ranges, stream-major):
+//   k_master_thr    one wave per (block, variant): the six calcBTHR() calls of
+//                   getStereoMaskThreshold (psychoac.py:540-562) incl. the
+//                   in-place Hann chains -> thr[gb][v][1024]
+//   k_master_front  one wave per block: LRMS decision (codec.py:94-102), MDCT
+//                   L/R + overall scale (codec.py:237-246), M/S lines, MLD
+//                   combination and per-band SMR selection (psychoac.py:533-682)
+//   k_master_tail   one wave per STREAM, blocks in order: withdrawBits, the two
+//                   BitAlloc calls with the extraBits carry (codec.py:222-260,
+//                   bitalloc.py:129-184), scale factors, 10-table Huffman
+//                   length scoring and depositBits (codec.py:111-124)
+//   k_master_pack   one wave per channel-block: sign bits, Huffman codes and
+//                   LRMS packed MSB-first (pacfile.py:288-351)
+
+struct PacMasterWork {
+    double* thr;        // [Bc][6][1024]
+    double* lines;      // [Bc][2][1024]  LRMSmdctLines
+    double* smr;        // [Bc][2][25]
+    double* bandpeak;   // [Bc][2][25]
+    uint8_t* lrms;      // [Bc][25]
+    uint8_t* overall;   // [Bc][2]
+    uint8_t* ba;        // [Bc][2][25]
+    uint8_t* sf;        // [Bc][2][25]
+    uint8_t* tid;       // [Bc][2]
+    int32_t* nbytes;    // [Bc*2]
+};
+
+// LRMS-variant signals: the in-place window chains of EncodeDualChannel and
+// getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
+// M = (a+b)/2, S = (a-b)/2; v2 = M*hann, v3 = S*hann, v4 = (M*hann)*hann, ...
+__device__ __forceinline__ double variant_sample(const BlockRef& rL, const BlockRef& rR,
+                                                 const PacTables* __restrict__ T, int v, int i) {
+    const double h = T->hann[i];
+    if (v == 1) return __dmul_rn(__dmul_rn(sample(rR, i), T->sine[i]), h);
+    const double a = __dmul_rn(__dmul_rn(sample(rL, i), T->sine[i]), h);
+    if (v == 0) return a;
+    const double b = __dmul_rn(__dmul_rn(sample(rR, i), T->sine[i]), h);
+    double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
+    ms = __dmul_rn(ms, h);
+    if (v >= 4) ms = __dmul_rn(ms, h);
+    return ms;
+}
+
+__global__ __launch_bounds__(64) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
+                                                   PacMasterWork W, int64_t gb0) {
+    __shared__ double2 buf[1024];
+    const int lane = threadIdx.x;
+    const int64_t j = blockIdx.x / 6;          // block within the chunk
+    const int v = blockIdx.x % 6;
+    const BlockRef rL = locate(src, gb0 + j, 0);
+    const BlockRef rR = locate(src, gb0 + j, 1);
+    auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
+    wave_spectrum_mag(d, T, buf, lane);
+    int nm = wave_find_maskers(buf, T, v >= 4 ? 0.0 : 15.0, lane);
+    double thr[16];
+    wave_masking(reinterpret_cast<const Masker*>(buf), nm, T, lane, thr);
+    double* out = W.thr + (j * 6 + v) * PAC_HALFN;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[q * WAVE + lane] = thr[q];
+}
+
+// --- numpy pairwise summation of a complex vector (loops_utils.h.src) -------
+// element j of the summed vector is f(j) (complex); n = 2 * count (doubles)
+template <int D, class F>
+__device__ double2 np_csum(const F& f, int e0, int n) {
+    if (n < 8) {
+        double sr = 0., si = 0.;
+        for (int i = 0; i < n; i += 2) { double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
+        return make_double2(sr, si);
+    }
+    if (D == 0 || n <= 128) {
+        double r[8];
+        double2 z0 = f(e0), z1 = f(e0 + 1), z2 = f(e0 + 2), z3 = f(e0 + 3);
+        r[0] = z0.x; r[1] = z0.y; r[2] = z1.x; r[3] = z1.y;
+        r[4] = z2.x; r[5] = z2.y; r[6] = z3.x; r[7] = z3.y;
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8) {
+            int e = e0 + i / 2;
+            z0 = f(e); z1 = f(e + 1); z2 = f(e + 2); z3 = f(e + 3);
+            r[0] += z0.x; r[1] += z0.y; r[2] += z1.x; r[3] += z1.y;
+            r[4] += z2.x; r[5] += z2.y; r[6] += z3.x; r[7] += z3.y;
+        }
+        double sr = ((r[0] + r[2]) + (r[4] + r[6]));
+        double si = ((r[1] + r[3]) + (r[5] + r[7]));
+        for (; i < n; i += 2) { double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
+        return make_double2(sr, si);
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    double2 a = np_csum<(D > 0 ? D - 1 : 0)>(f, e0, n2);
+    double2 b = np_csum<(D > 0 ? D - 1 : 0)>(f, e0 + n2 / 2, n - n2);
+    return make_double2(a.x + b.x, a.y + b.y);
+}
+
+// complex spectrum X[k], k < 1024, of a real 2048-block into buf (in place)
+template <class DS>
+__device__ __forceinline__ void wave_spectrum_cplx(const DS& d, const PacTables* __restrict__ T,
+                                                   double2* buf, int lane) {
+#pragma unroll 4
+    for (int n0 = 0; n0 < 1024; n0 += WAVE) {
+        int n = n0 + lane;
+        buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
+    }
+    wave_fft<10>(buf, T->fft_tw, lane);
+#pragma unroll
+    for (int t0 = 0; t0 <= 512; t0 += WAVE) {
+        int k = t0 + lane;
+        if (k > 512) continue;
+        int k2 = (1024 - k) & 1023;
+        double2 Za = buf[k], Zb = buf[k2];
+        double2 X[2];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            int kk = side ? k2 : k;
+            double2 A = side ? Zb : Za;
+            double2 Bc = side ? Za : Zb;
+            double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
+            double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
+            double2 wo = cmul(T->rfft_tw[kk], o);
+            X[side] = make_double2(e.x + wo.y, e.y - wo.x);
+        }
+        buf[k] = X[0];
+        if (k2 != k) buf[k2] = X[1];
+    }
+    wave_sync();
+}
+
+__global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTables* __restrict__ T,
+                                                     PacMasterWork W, int64_t gb0) {
+    __shared__ double2 bufL[1024];      // 16 KB
+    __shared__ double2 bufR[1024];      // 16 KB
+    __shared__ uint8_t lrms_s[PAC_NB];
+    const int lane = threadIdx.x;
+    const int64_t j = blockIdx.x;
+    const BlockRef rL = locate(src, gb0 + j, 0);
+    const BlockRef rR = locate(src, gb0 + j, 1);
+
+    // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:96-102)
+    wave_spectrum_cplx([&](int i) { return sample(rL, i); }, T, bufL, lane);
+    wave_spectrum_cplx([&](int i) { return sample(rR, i); }, T, bufR, lane);
+    if (lane < PAC_NB) {
+        const int lo = T->lower[lane], m = T->nlines[lane];
+        auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
+            return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
+                                __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
+        };
+        auto fd = [&](int e) {
+            double2 a = sq(bufL[lo + e]), b = sq(bufR[lo + e]);
+            return make_double2(__dsub_rn(a.x, b.x), __dsub_rn(a.y, b.y));
+        };
+        auto fs = [&](int e) {
+            double2 a = sq(bufL[lo + e]), b = sq(bufR[lo + e]);
+            return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
+        };
+        double2 sd = np_csum<5>(fd, 0, 2 * m);
+        double2 ss = np_csum<5>(fs, 0, 2 * m);
+        int v = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
+        lrms_s[lane] = (uint8_t)v;
+        W.lrms[j * PAC_NB + lane] = (uint8_t)v;
+    }
+    wave_sync();
+
+    // --- MDCT L and R, overall scale factors -------------------------------
+    double* XL = reinterpret_cast<double*>(bufL + 512);
+    double* XR = reinterpret_cast<double*>(bufR + 512);
+    wave_mdct([&](int i) { return __dmul_rn(sample(rL, i), T->sine[i]); }, T, bufL, XL, lane);
+    wave_mdct([&](int i) { return __dmul_rn(sample(rR, i), T->sine[i]); }, T, bufR, XR, lane);
+    double mxL = 0.0, mxR = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        mxL = fmax(mxL, fabs(XL[q * WAVE + lane]));
+        mxR = fmax(mxR, fabs(XR[q * WAVE + lane]));
+    }
+    const int oL = pac_scale_factor(wave_max(mxL), 5);
+    const int oR = pac_scale_factor(wave_max(mxR), 5);
+    const double gL = (double)(1 << oL), gR = (double)(1 << oR);
+    const double offL = 6.02 * oL, offR = 6.02 * oR;
+    if (lane == 0) { W.overall[j * 2] = (uint8_t)oL; W.overall[j * 2 + 1] = (uint8_t)oR; }
+
+    // --- per-line SMR terms (psychoac.py:533-597) ---------------------------
+    double* dLR0 = reinterpret_cast<double*>(bufL);     // first 8 KB of each buffer
+    double* dLR1 = reinterpret_cast<double*>(bufR);
+    const double* thr = W.thr + j * 6 * PAC_HALFN;
+    double* lines = W.lines + j * 2 * PAC_HALFN;
+    double dM[16], dS[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int l = q * WAVE + lane;
+        double xl = __dmul_rn(XL[l], gL), xr = __dmul_rn(XR[l], gR);
+        double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
+        double splL = pac_spl(4. * (xl * xl)) - offL;
+        double splR = pac_spl(4. * (xr * xr)) - offR;
+        double splM = pac_spl(4. * (M * M)) - offL;
+        double splS = pac_spl(4. * (S * S)) - offR;
+        double bL = thr[0 * PAC_HALFN + l], bR = thr[1 * PAC_HALFN + l];
+        double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
+        double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
+        double mld = T->mld[l];
+        double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
+        double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
+        double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
+        double c = bM < mldM ? bM : mldM;
+        double thrS = bS > c ? bS : c;
+        dM[q] = splM - thrM;
+        dS[q] = splS - thrS;
+        int ms = lrms_s[T->band_of_line[l]];
+        lines[l] = ms ? M : xl;
+        lines[PAC_HALFN + l] = ms ? S : xr;
+        // stash L/R terms where the MDCT scratch was
+        XL[l] = splL - bL;      // XL/XR no longer needed once read above
+        XR[l] = splR - bR;
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int l = q * WAVE + lane;
+        dLR0[l] = dM[q];
+        dLR1[l] = dS[q];
+    }
+    wave_sync();
+    if (lane < PAC_NB) {
+        const int lo = T->lower[lane], n = T->nlines[lane];
+        const int ms = lrms_s[lane];
+        double s0 = -INFINITY, s1 = -INFINITY, p0 = 0.0, p1 = 0.0;
+        for (int l = lo; l < lo + n; ++l) {
+            s0 = fmax(s0, ms ? dLR0[l] : XL[l]);
+            s1 = fmax(s1, ms ? dLR1[l] : XR[l]);
+            p0 = fmax(p0, fabs(lines[l]));
+            p1 = fmax(p1, fabs(lines[PAC_HALFN + l]));
+        }
+        if (n == 0) { s0 = -96.0; s1 = -96.0; }
+        W.smr[(j * 2 + 0) * PAC_NB + lane] = s0;
+        W.smr[(j * 2 + 1) * PAC_NB + lane] = s1;
+        W.bandpeak[(j * 2 + 0) * PAC_NB + lane] = p0;
+        W.bandpeak[(j * 2 + 1) * PAC_NB + lane] = p1;
+    }
+}
+
+// --- master BitAlloc (bitalloc.py:129-184), evaluated identically by every lane
+__device__ long bitalloc_master(const double* __restrict__ smr_g, const uint8_t* lrms,
+                                const PacTables* __restrict__ T, double bitBudget, long extra,
+                                int maxMantBits, int bits_out[PAC_NB]) {
+    double smr[PAC_NB];
+    int bits[PAC_NB], nl[PAC_NB], lr[PAC_NB];
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        smr[b] = smr_g[b];
+        bits[b] = 0;
+        nl[b] = T->nlines[b];
+        lr[b] = lrms[b];
+    }
+    unsigned valid = (1u << PAC_NB) - 1u;
+    long total = (long)(bitBudget + (double)extra);
+    while (valid) {
+        int im = -1;
+        double best = 0.0;
+        double g = smr[0] - (bits[0] - 1) * 6.;
+#pragma unroll
+        for (int b = 0; b < PAC_NB; ++b) {
+            double v = smr[b] - bits[b] * 6.;
+            if (((valid >> b) & 1u) && (im < 0 || v > best)) { best = v; im = b; }
+            double w = smr[b] - (bits[b] - 1) * 6.;
+            g = w > g ? w : g;
+        }
+        int nli = 0, lri = 0, bi = 0;
+#pragma unroll
+        for (int b = 0; b < PAC_NB; ++b)
+            if (b == im) { nli = nl[b]; lri = lr[b]; bi = bits[b]; }
+        const unsigned bit = 1u << im;
+        if (g < (lri ? -5.0 : -15.0)) valid &= ~bit;
+        if (total - nli >= 0) {
+#pragma unroll
+            for (int b = 0; b < PAC_NB; ++b)
+                if (b == im) bits[b] += 1;
+            total -= nli;
+            if (bi + 1 >= maxMantBits) valid &= ~bit;
+        } else {
+            valid &= ~bit;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        if (bits[b] == 1) { total += nl[b]; bits[b] = 0; }
+        bits_out[b] = bits[b];
+    }
+    return total - extra;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+
+// One wave per stream: the serial reservoir chain over the stream's blocks.
+__global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict__ T,
+                                                    const PacHuffTables* __restrict__ H,
+                                                    PacMasterWork W, const int64_t* __restrict__ blk_off,
+                                                    int s0, int64_t gb0, int64_t gb1,
+                                                    int64_t* __restrict__ st_extra,
+                                                    int64_t* __restrict__ st_deposit, double bitBudget) {
+    __shared__ int ba_s[PAC_NB], sf_s[PAC_NB];
+    const int lane = threadIdx.x;
+    const int s = s0 + blockIdx.x;
+    int64_t b_begin = blk_off[s] > gb0 ? blk_off[s] : gb0;
+    int64_t b_end = blk_off[s + 1] < gb1 ? blk_off[s + 1] : gb1;
+    long extra = st_extra[s], deposit = st_deposit[s];
+    for (int64_t gb = b_begin; gb < b_end; ++gb) {
+        const int64_t j = gb - gb0;
+        // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
+        long e = 0;
+        if (deposit > 10) { e = deposit / 100; deposit -= e; }
+        else if (deposit < 0) { e = deposit; deposit = 0; }
+        extra += e;
+        long dep_add = 0;
+        for (int ch = 0; ch < 2; ++ch) {
+            int bits[PAC_NB];
+            long diff = bitalloc_master(W.smr + (j * 2 + ch) * PAC_NB, W.lrms + j * PAC_NB, T,
+                                        bitBudget, extra, 16, bits);
+            extra += diff;
+            if (lane < PAC_NB) {
+                int ba = 0;
+#pragma unroll
+                for (int b = 0; b < PAC_NB; ++b)
+                    if (b == lane) ba = bits[b];
+                ba_s[lane] = ba;
+                int sf = pac_scale_factor(W.bandpeak[(j * 2 + ch) * PAC_NB + lane], ba);
+                sf_s[lane] = sf;
+                W.ba[(j * 2 + ch) * PAC_NB + lane] = (uint8_t)ba;
+                W.sf[(j * 2 + ch) * PAC_NB + lane] = (uint8_t)sf;
+            }
+            wave_sync();
+            // StripSignBits + Huffman.encodeData scoring of the 10 tables
+            const double* ln = W.lines + (j * 2 + ch) * PAC_HALFN;
+            int acc[PAC_NTAB];
+#pragma unroll
+            for (int t = 0; t < PAC_NTAB; ++t) acc[t] = 0;
+            int nsign = 0, orig = 0;
+            for (int q = 0; q < 16; ++q) {
+                int l = q * WAVE + lane;
+                int b = T->band_of_line[l];
+                int ba = ba_s[b];
+                if (!ba) continue;
+                uint32_t m = pac_mantissa(ln[l], sf_s[b], ba);
+                uint32_t sym = m & ((1u << (ba - 1)) - 1u);
+                nsign += 1;
+                orig += ba;
+#pragma unroll
+                for (int t = 0; t < PAC_NTAB; ++t) {
+                    int L = H->len[t][sym];
+                    acc[t] += L ? L : H->esc_len[t] + ba;
+                }
+            }
+            nsign = wave_sum_i(nsign);
+            orig = wave_sum_i(orig);
+            int best = 0, bestid = 1;
+#pragma unroll
+            for (int t = 0; t < PAC_NTAB; ++t) {
+                int v = wave_sum_i(acc[t]);
+                if (t == 0 || v < best) { best = v; bestid = t + 1; }
+            }
+            dep_add += (long)orig - ((long)best + nsign + 4);
+            int nbits = 8 + 8 * PAC_NB + nsign + best + PAC_NB;
+            if (lane == 0) {
+                W.tid[j * 2 + ch] = (uint8_t)bestid;
+                W.nbytes[j * 2 + ch] = 4 + (nbits + 7) / 8;
+            }
+            wave_sync();
+        }
+        deposit += dep_add;     // depositBits per channel (codec.py:120)
+    }
+    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
+}
+
+__device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    *total = __shfl(x, 63, WAVE);
+    return x - v;
+}
+
+// One wave per channel-block g = 2*j + ch of the chunk.
+__global__ __launch_bounds__(64) void k_master_pack(const PacTables* __restrict__ T,
+                                                    const PacHuffTables* __restrict__ H,
+                                                    PacMasterWork W, const int64_t* __restrict__ off,
+                                                    const int64_t* __restrict__ base,
+                                                    uint8_t* __restrict__ out) {
+    __shared__ uint32_t words[PACK_WORDS];
+    __shared__ int bas[PAC_NB], sfs[PAC_NB], bstart[PAC_NB + 1];
+    __shared__ int rowsum[16];
+    const int lane = threadIdx.x;
+    const int64_t g = blockIdx.x;
+    const int64_t j = g >> 1;
+    const int ch = (int)(g & 1);
+    for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
+    if (lane < PAC_NB) {
+        bas[lane] = W.ba[g * PAC_NB + lane];
+        sfs[lane] = W.sf[g * PAC_NB + lane];
+    }
+    wave_sync();
+    const int tid = W.tid[g] - 1;
+    const double* ln = W.lines + g * PAC_HALFN;
+    // per line: sign + code of length clen (0 for ba == 0 bands)
+    uint32_t code[16], sgn[16];
+    int clen[16], esc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int l = q * WAVE + lane;
+        int b = T->band_of_line[l];
+        int ba = bas[b];
+        clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
+        if (ba) {
+            uint32_t m = pac_mantissa(ln[l], sfs[b], ba);
+            uint32_t sym = m & ((1u << (ba - 1)) - 1u);
+            sgn[q] = (m >> (ba - 1)) & 1u;
+            int L = H->len[tid][sym];
+            if (L) { clen[q] = L; code[q] = H->bits[tid][sym]; }
+            else { clen[q] = H->esc_len[tid] + ba; esc[q] = 1; code[q] = sym; }
+        }
+    }
+    // exclusive prefix of code lengths in line order (row q holds lines 64q..64q+63)
+    int pre[16];
+    int run = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int tot;
+        int ex = wave_excl_scan_i(clen[q], lane, &tot);
+        pre[q] = run + ex;
+        run += tot;
+    }
+    // band starts: 8 + sum_{b'<b} (8 + [ba>0](nl + codebits_b'))
+    if (lane == 0) {
+        int p = 8;
+        for (int b = 0; b < PAC_NB; ++b) { bstart[b] = p; p += 8; if (bas[b]) p += T->nlines[b]; }
+        bstart[PAC_NB] = p;   // LRMS bits start (minus all code bits, added below)
+    }
+    // code bits of all earlier bands: codebits before line lower[b] = pre at that line
+    __shared__ int pre_at_lower[PAC_NB];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int l = q * WAVE + lane;
+        int b = T->band_of_line[l];
+        if (l == T->lower[b]) pre_at_lower[b] = pre[q];
+    }
+    wave_sync();
+    if (lane == 0) {
+        put_bits(words, 0, (uint32_t)W.overall[g], 4);
+        put_bits(words, 4, (uint32_t)(tid + 1), 4);
+    }
+    if (lane < PAC_NB) {
+        int b = lane, ba = bas[b];
+        int p = bstart[b] + pre_at_lower[b];
+        put_bits(words, p, (uint32_t)(ba ? ba - 1 : 0), 4);
+        put_bits(words, p + 4, (uint32_t)sfs[b], 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        int l = q * WAVE + lane;
+        int b = T->band_of_line[l];
+        int ba = bas[b];
+        if (!ba) continue;
+        int p0 = bstart[b] + pre_at_lower[b] + 8;
+        put_bits(words, p0 + (l - T->lower[b]), sgn[q], 1);
+        int pc = p0 + T->nlines[b] + (pre[q] - pre_at_lower[b]);
+        if (esc[q]) {
+            int el = H->esc_len[tid];
+            put_bits(words, pc, H->esc_bits[tid], el);
+            put_bits(words, pc + el, code[q], ba);
+        } else {
+            put_bits(words, pc, code[q], clen[q]);
+        }
+    }
+    if (lane < PAC_NB) {
+        int p = bstart[PAC_NB] + run + lane;
+        put_bits(words, p, (uint32_t)W.lrms[j * PAC_NB + lane], 1);
+    }
+    wave_sync();
+    const int nbytes = W.nbytes[g] - 4;
+    store_block_bytes(out + *base + off[g], words, nbytes, lane);
+}
+
+__global__ void k_add_base(int64_t* __restrict__ base, const int64_t* __restrict__ total) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *base += *total;
+}
+
+// stream start offsets for streams whose first block lies in [gb0, gb1)
+__global__ void k_master_stream_offsets(const int64_t* __restrict__ off, const int64_t* __restrict__ blk_off,
+                                        int n_streams, int64_t gb0, int64_t gb1,
+                                        const int64_t* __restrict__ base, int64_t* __restrict__ so) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    int64_t b = blk_off[s];
+    if (b >= gb0 && b < gb1) so[s] = *base + off[(b - gb0) * 2];
+}

@@ -1,0 +1,139 @@
+"""GPU parity of the master profile (codec/: M/S, Huffman, bit reservoir)
+against the committed .wak fixture, the reference-generated goldens and the CPU
+oracle.  Bar: bit-exact bytes and reservoir state."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, fixture
+
+import pac_amd  # noqa: F401
+from pac_amd import pacfile, _lib, synth
+import pyoracle as P
+
+pytestmark = pytest.mark.gpu
+MASTER = pacfile.PROFILE_MASTER
+
+
+def test_piano_test2_wak_bit_exact(ctx):
+    """coded/piano_test2.wak (reference fixture) byte for byte."""
+    got = pacfile.encode_file(fixture("piano_test2.wav"), profile=MASTER, context=ctx)
+    with open(fixture("piano_test2.wak"), "rb") as f:
+        ref = f.read()
+    assert len(got) == len(ref)
+    assert got == ref
+
+
+@pytest.mark.parametrize("name", ["master_pinktones48k", "master_zero48k", "master_square44k",
+                                  "master_white48k"])
+def test_golden_reference_streams(ctx, name):
+    pcm = np.load(os.path.join(GOLD, name + ".in.npy"))
+    with open(os.path.join(GOLD, name + ".wak"), "rb") as f:
+        ref = f.read()
+    fs = {"48k": 48000, "44k": 44100}[name[-3:]]
+    body = pacfile.encode_streams([pcm], fs, MASTER, context=ctx)[0]
+    assert pacfile.header_bytes(fs, 2, pcm.shape[0]) + body == ref
+
+
+def test_harpsichord_master_vs_oracle(ctx):
+    """harpsichord.wav through the master coder (no committed golden for it;
+    the oracle is pinned on 13 master fixtures)."""
+    fs, nch, n, pcm = P.read_wav(fixture("harpsichord.wav"))
+    got = pacfile.encode_streams([pcm], fs, MASTER, context=ctx)[0]
+    o = P.Oracle(fs, huffman=True)
+    assert got == o.encode_data(P.MASTER, pcm)
+
+
+@pytest.mark.parametrize("fs", [48000, 44100])
+def test_multi_stream_vs_oracle_and_state(ctx, fs):
+    """Independent streams in one call (each with its own reservoir), ragged
+    lengths, plus the returned reservoir state (extraBits, bitDeposit)."""
+    lens = [0, 1023, 1024, 3000, 15 * 1024 + 5, 40 * 1024]
+    streams = [synth.pink_tones_pcm(n, fs, seed=i + 3) if i % 2 else synth.white_pcm(n, 2, seed=i)
+               for i, n in enumerate(lens)]
+    states = [_lib.StreamState() for _ in lens]
+    got = pacfile.encode_streams(streams, fs, MASTER, context=ctx, states=states)
+    o = P.Oracle(fs, huffman=True)
+    for i, s in enumerate(streams):
+        st = P.State()
+        exp = o.encode_data(P.MASTER, s, state=st)
+        assert got[i] == exp, "stream %d differs" % i
+        assert (states[i].extra_bits, states[i].bit_deposit) == (st.extraBits, st.deposit)
+
+
+def test_chunking_invariance(ctx):
+    """Chunked processing (reservoir carried across chunk boundaries in the
+    middle of a stream) gives the same bytes."""
+    fs = 48000
+    streams = [synth.pink_tones_pcm(37 * 1024 + 11, fs, seed=5), synth.white_pcm(20 * 1024, 2, seed=6)]
+    full = pacfile.encode_streams(streams, fs, MASTER, context=ctx)
+    lib = ctx.L
+    import ctypes as C
+    small = _lib.Context(0)
+    try:
+        small_set = getattr(lib, "pac_set_chunk_blocks")
+        small_set.argtypes = [C.c_void_p, C.c_int64]
+        small_set(small.h, 7)
+        chunked = pacfile.encode_streams(streams, fs, MASTER, context=small)
+    finally:
+        small.close()
+    assert chunked == full
+
+
+def test_plugin_surface_per_block_matches(ctx, tmp_path):
+    """PACFile.WriteDataBlock per hop with the Huffman reservoir object, as the
+    reference driver runs it (pacfile.py:474-499), equals the fixture prefix."""
+    from pac_amd.pcmfile import PCMFile
+    from pac_amd.huffman import Huffman
+    huffman = Huffman()
+    out = tmp_path / "p.wak"
+    inFile = PCMFile(fixture("piano_test2.wav"))
+    outFile = pacfile.PACFile(str(out), profile=MASTER, context=ctx)
+    cp = inFile.OpenForReading()
+    cp.nMDCTLines, cp.nScaleBits, cp.nMantSizeBits = 1024, 4, 4
+    cp.targetBitsPerSample, cp.nTableIDBits = 2.27, 4
+    cp.nSamplesPerBlock = cp.nMDCTLines
+    outFile.OpenForWriting(cp)
+    for _ in range(30):
+        data = inFile.ReadDataBlock(cp)
+        if not data:
+            break
+        outFile.WriteDataBlock(data, cp, huffman)
+    outFile.fp.close()
+    got = out.read_bytes()
+    with open(fixture("piano_test2.wak"), "rb") as f:
+        ref = f.read()
+    assert got == ref[:len(got)]
+
+
+def test_codec_encode_tuple_master(ctx):
+    """codec.Encode (codec.py:83-129) tuple fields vs the oracle for a block."""
+    from pac_amd import codec
+    from pac_amd.audiofile import CodingParams
+    from pac_amd.huffman import Huffman
+    from pac_amd.psychoac import ScaleFactorBands, AssignMDCTLinesFromFreqLimits
+    from pac_amd.pcmfile import codes_to_float
+    fs = 48000
+    pcm = synth.pink_tones_pcm(4 * 1024, fs, seed=9)
+    x = [codes_to_float(pcm[1024:3072, c]) for c in range(2)]
+    cp = CodingParams()
+    cp.sampleRate, cp.nChannels, cp.nMDCTLines = fs, 2, 1024
+    cp.nScaleBits, cp.nMantSizeBits, cp.targetBitsPerSample, cp.nTableIDBits = 4, 4, 2.27, 4
+    cp.sfBands = ScaleFactorBands(AssignMDCTLinesFromFreqLimits(1024, fs))
+    cp.extraBits = 17
+    h = Huffman()
+    h.bitDeposit = 1234
+    sf, ba, signs, codes, tid, overall, lrms = codec.Encode(x, cp, h, profile=codec.PROFILE_MASTER,
+                                                            context=ctx)
+    o = P.Oracle(fs, huffman=True)
+    st = P.State()
+    st.extraBits, st.deposit = 17, 1234
+    ob = o.block_master(x[0], x[1], st)
+    assert list(lrms) == list(ob.lrms)
+    assert (cp.extraBits, h.bitDeposit) == (st.extraBits, st.deposit)
+    for c in range(2):
+        assert overall[c] == ob.overall[c]
+        assert tid[c] == ob.table_id[c]
+        assert list(ba[c]) == list(ob.ba[c])
+        assert list(sf[c]) == list(ob.sf[c])

@@ -1,0 +1,220 @@
+"""CPU-only tests of the host side: the C-ABI library loads and exports every
+symbol include/pac_gpu.h declares (no compute without a GPU), host mirrors of
+the reference's file-format logic, the Huffman table export, the synthetic
+generators and the stream shard planner (gloo, world_size 2)."""
+import ctypes as C
+import os
+import re
+import struct
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, REF, ROOT, fixture
+
+import pac_amd  # noqa: F401
+from pac_amd import _lib, pacfile, pcmfile, psychoac, shard, synth
+from pac_amd.huffman import Huffman, load_tables
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "pac_gpu.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(pac_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(L, s), s
+    assert L.pac_version() >= 100
+
+
+def test_nm_exports_are_extern_c():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (pac_[a-z_0-9]+)$", out, re.M))
+    assert set(header_symbols()) <= exported
+
+
+def test_no_gpu_errors_are_loud():
+    """Without a GPU the context refuses (no silent CPU fallback)."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    rc = L.pac_ctx_create(0, C.byref(h))
+    if rc == 0:
+        L.pac_ctx_destroy(h)
+        pytest.skip("a GPU is present")
+    assert rc == -2
+    assert b"device" in L.pac_last_error().lower() or b"hip" in L.pac_last_error().lower()
+
+
+@pytest.mark.parametrize("fs", [8000, 16000, 22050, 32000, 44100, 48000, 96000])
+def test_band_layout_host_equals_abi(fs):
+    assert psychoac.AssignMDCTLinesFromFreqLimits(1024, fs) == list(_lib.band_layout(fs))
+    assert sum(psychoac.AssignMDCTLinesFromFreqLimits(1024, fs)) <= 1024
+
+
+def test_band_layouts_match_survey():
+    assert psychoac.AssignMDCTLinesFromFreqLimits(1024, 44100) == [
+        5, 4, 5, 5, 5, 5, 7, 7, 7, 9, 10, 11, 13, 15, 17, 21, 26, 32, 42, 51, 61, 83, 116, 163, 304]
+    assert psychoac.AssignMDCTLinesFromFreqLimits(1024, 48000) == [
+        4, 5, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 12, 14, 16, 19, 24, 30, 38, 47, 56, 76, 107, 149, 363]
+
+
+def test_header_quirk():
+    """pacfile.py:240-242: only exact multiples of 1024 are bumped."""
+    h = pacfile.header_bytes(44100, 2, 102400)
+    assert struct.unpack("<LHLLHH", h[4:22])[2] == 103424
+    h = pacfile.header_bytes(44100, 2, 102401)
+    assert struct.unpack("<LHLLHH", h[4:22])[2] == 102401
+    with open(fixture("harpsichord.pac"), "rb") as f:
+        ref = f.read()
+    assert pacfile.header_bytes(44100, 2, 394646) == ref[:len(pacfile.header_bytes(44100, 2, 394646))]
+
+
+def test_pcm_reader_matches_reference_conversion():
+    cp, frames = pcmfile.read_for_encode(fixture("harpsichord.wav"))
+    assert (cp.sampleRate, cp.nChannels, cp.numSamples) == (44100, 2, 394646)
+    assert frames.shape == (394646, 2)
+    x = pcmfile.codes_to_float(np.array([-32768, -32767, -1, 0, 1, 32767]))
+    assert np.signbit(x[0]) == False and x[0] == 0.0          # the -32768 quirk
+    assert x[1] == -(2.0 * 32767 / 65535.0) and x[5] == 2.0 * 32767 / 65535.0
+    assert x[2] == -(2.0 / 65535.0) and x[3] == 0.0
+
+
+def test_pcmfile_hop_reads_equal_bulk(tmp_path):
+    """PCMFile.ReadDataBlock hop by hop == read_for_encode (zero-padded tail)."""
+    pcm = synth.white_pcm(3 * 1024 + 5, 2, seed=3)
+    p = tmp_path / "x.wav"
+    with open(p, "wb") as f:
+        d = pcm.astype("<i2").tobytes()
+        f.write(struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + len(d), b"WAVE", b"fmt ", 16, 1, 2,
+                            48000, 48000 * 4, 4, 16, b"data", len(d)) + d)
+    pf = pcmfile.PCMFile(str(p))
+    cp = pf.OpenForReading()
+    cp.nSamplesPerBlock = 1024
+    hops = []
+    while True:
+        blk = pf.ReadDataBlock(cp)
+        if blk is None:
+            break
+        hops.append(np.stack(blk, 1))
+    pf.Close(cp)
+    assert len(hops) == 4
+    _, frames = pcmfile.read_for_encode(str(p))
+    whole = np.concatenate(hops)[: frames.shape[0]]
+    assert np.array_equal(whole, pcmfile.codes_to_float(frames))
+    assert np.all(np.concatenate(hops)[frames.shape[0]:] == 0)
+
+
+def test_exact_multiple_reads_trailing_chunk(tmp_path):
+    """numSamples % 1024 == 0: the bumped header count makes the reference
+    reader take one more hop from the bytes after the data chunk."""
+    pcm = synth.white_pcm(2 * 1024, 2, seed=4)
+    p = tmp_path / "y.wav"
+    tail = b"LIST\x04\x00\x00\x00abcd"
+    with open(p, "wb") as f:
+        d = pcm.astype("<i2").tobytes()
+        f.write(struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + len(d) + len(tail), b"WAVE", b"fmt ",
+                            16, 1, 2, 48000, 48000 * 4, 4, 16, b"data", len(d)) + d + tail)
+    _, frames = pcmfile.read_for_encode(str(p))
+    assert frames.shape[0] == 3 * 1024
+    assert np.array_equal(frames[:2048], pcm)
+    raw = np.frombuffer(tail + b"\0" * (4096 - len(tail)), "<i2").reshape(-1, 2)
+    assert np.array_equal(frames[2048:], raw)
+
+
+def test_float_to_codes_roundtrip():
+    c = np.arange(-32767, 32768, 7, dtype=np.int16)
+    assert np.array_equal(pcmfile.float_to_codes(pcmfile.codes_to_float(c)), c)
+
+
+def test_huffman_tables_image():
+    t = load_tables()
+    assert sorted(t) == list(range(1, 11))
+    assert len(t[5]) == 4492 and len(t[8]) == 67
+    for tid, enc in t.items():
+        codes = sorted(enc.values(), key=len)
+        # prefix-free
+        s = set()
+        for c in codes:
+            assert not any(c[:k] in s for k in range(1, len(c) + 1)), (tid, c)
+            s.add(c)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+def test_huffman_export_matches_pickle_stream():
+    """Re-export from the reference pickle (opcode-walk, nothing executed)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import export_huffman_tables as ex
+    with open(ex.REF, "rb") as f:
+        root = ex.parse_protocol0(f.read())
+    t = load_tables()
+    for tid in range(1, 11):
+        assert root[tid].state["encodingTable"] == t[tid]
+
+
+def test_huffman_reservoir_semantics():
+    """withdrawBits (Huffman.py:363-371) with Python-2 floor division."""
+    h = Huffman()
+    h.depositBits(1234)
+    assert h.withdrawBits() == 12 and h.getBitDeposit() == 1222
+    h.bitDeposit = 10
+    assert h.withdrawBits() == 0 and h.bitDeposit == 10
+    h.bitDeposit = -37
+    assert h.withdrawBits() == -37 and h.bitDeposit == 0
+
+
+def test_hash_white_mirror_is_gaussian():
+    x = synth.hash_white_pcm(200000, 1234).astype(np.float64) / (0.25 * 32767)
+    assert abs(x.mean()) < 0.01 and abs(x.std() - 1) < 0.01
+
+
+def test_shard_plan_lpt():
+    counts = [1001, 5, 300, 300, 2000, 7, 1001]
+    sh = shard.plan(counts, 3)
+    assert sorted(i for s in sh for i in s) == list(range(len(counts)))
+    loads, imb = shard.balance(counts, sh)
+    assert loads.max() == 2000      # the single longest stream bounds the makespan
+    assert shard.plan(counts, 1) == [list(range(len(counts)))]
+    assert shard.blocks_of(0) == 1 and shard.blocks_of(1024) == 2 and shard.blocks_of(1025) == 3
+
+
+GLOO_WORKER = r"""
+import os, sys
+sys.path.insert(0, %r)
+import torch.distributed as td
+import pac_amd
+from pac_amd import shard
+td.init_process_group("gloo")
+r, w = td.get_rank(), td.get_world_size()
+counts = [shard.blocks_of(n) for n in (5000, 1, 40000, 123456, 7777, 1024 * 1000, 3, 99999)]
+mine = shard.plan(counts, w)[r]
+allp = [None] * w
+td.all_gather_object(allp, mine)
+flat = sorted(i for p in allp for i in p)
+assert flat == list(range(len(counts))), flat
+assert all(set(allp[a]).isdisjoint(allp[b]) for a in range(w) for b in range(a + 1, w))
+td.barrier()
+if r == 0:
+    print("GLOO_OK", allp)
+td.destroy_process_group()
+"""
+
+
+def test_shard_plan_gloo_world2(tmp_path):
+    """The N>1 path: every rank derives the same plan; shards are disjoint and
+    cover all streams (gloo all_gather on CPU, world_size 2)."""
+    script = tmp_path / "w.py"
+    script.write_text(GLOO_WORKER % ROOT)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", "29517",
+                        str(script)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "GLOO_OK" in r.stdout

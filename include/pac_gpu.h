@@ -132,6 +132,14 @@ int pac_set_timing(pac_ctx *ctx, int32_t enable);
 /* Stereo blocks per master-profile chunk (device scratch ~65 KB/block). */
 int pac_set_chunk_blocks(pac_ctx *ctx, int64_t blocks);
 int pac_last_timing(pac_ctx *ctx, pac_timing *out);
+/* Parity probe: calcBTHR (psychoac.py:409-456) of n blocks of 2048 float64
+ * samples as the reference receives them (Hann applied inside): the masking
+ * threshold per MDCT line and the masker count. */
+int pac_debug_threshold(pac_ctx *ctx, int32_t sample_rate, int32_t n, const double *data,
+                        int32_t no_drop, double *thr, int32_t *npeaks);
+/* Parity probe: SineWindow + MDCT (window.py:27-39, mdct.py:49-82) of n raw
+ * 2048-sample blocks -> 1024 lines each (before the overall scale). */
+int pac_debug_mdct(pac_ctx *ctx, int32_t n, const double *data, double *X);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,8 @@ def lib():
         "pac_set_timing": (C.c_int, [vp, i32]),
         "pac_set_chunk_blocks": (C.c_int, [vp, i64]),
         "pac_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
+        "pac_debug_threshold": (C.c_int, [vp, i32, i32, vp, i32, vp, vp]),
+        "pac_debug_mdct": (C.c_int, [vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -200,6 +202,21 @@ class Context:
 
     def synth_white(self, dev_pcm, n_samples, seed):
         check(self.L.pac_synth_white(self.h, dev_pcm, int(n_samples), int(seed)))
+
+    def debug_threshold(self, sample_rate, data, no_drop=False):
+        d = np.ascontiguousarray(np.atleast_2d(data), dtype=np.float64)
+        n = d.shape[0]
+        thr = np.zeros((n, 1024))
+        npk = np.zeros(n, dtype=np.int32)
+        check(self.L.pac_debug_threshold(self.h, int(sample_rate), n, d.ctypes.data, int(no_drop),
+                                         thr.ctypes.data, npk.ctypes.data))
+        return thr, npk
+
+    def debug_mdct(self, data):
+        d = np.ascontiguousarray(np.atleast_2d(data), dtype=np.float64)
+        X = np.zeros((d.shape[0], 1024))
+        check(self.L.pac_debug_mdct(self.h, d.shape[0], d.ctypes.data, X.ctypes.data))
+        return X
 
     def sync(self):
         check(self.L.pac_sync(self.h))

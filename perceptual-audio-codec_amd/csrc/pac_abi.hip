@@ -741,6 +741,46 @@ extern "C" int pac_set_timing(pac_ctx* c, int32_t enable) {
     c->timing = enable != 0;
     return PAC_OK;
 }
+extern "C" int pac_debug_threshold(pac_ctx* c, int32_t sample_rate, int32_t n, const double* data,
+                                   int32_t no_drop, double* thr, int32_t* npeaks) {
+    int rc;
+    if (!c || !data || !thr || !npeaks || n < 1) return set_err(PAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, sample_rate, &T))) return rc;
+    double *dd = nullptr, *dt = nullptr;
+    int32_t* dp = nullptr;
+    HIPCHK(hipMalloc((void**)&dd, (size_t)n * PAC_N * sizeof(double)));
+    HIPCHK(hipMalloc((void**)&dt, (size_t)n * PAC_HALFN * sizeof(double)));
+    HIPCHK(hipMalloc((void**)&dp, (size_t)n * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(dd, data, (size_t)n * PAC_N * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_threshold, dim3(n), dim3(64), 0, c->stream, T, dd, no_drop, dt, dp);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(thr, dt, (size_t)n * PAC_HALFN * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(npeaks, dp, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    hipFree(dd); hipFree(dt); hipFree(dp);
+    return PAC_OK;
+}
+
+extern "C" int pac_debug_mdct(pac_ctx* c, int32_t n, const double* data, double* X) {
+    if (!c || !data || !X || n < 1) return set_err(PAC_E_ARG, "bad argument");
+    int rc;
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, 48000, &T))) return rc;
+    double *dd = nullptr, *dx = nullptr;
+    HIPCHK(hipMalloc((void**)&dd, (size_t)n * PAC_N * sizeof(double)));
+    HIPCHK(hipMalloc((void**)&dx, (size_t)n * PAC_HALFN * sizeof(double)));
+    HIPCHK(hipMemcpy(dd, data, (size_t)n * PAC_N * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_mdct, dim3(n), dim3(64), 0, c->stream, T, dd, dx);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(X, dx, (size_t)n * PAC_HALFN * sizeof(double), hipMemcpyDeviceToHost));
+    hipFree(dd); hipFree(dx);
+    return PAC_OK;
+}
+
 extern "C" int pac_set_chunk_blocks(pac_ctx* c, int64_t blocks) {
     if (!c || blocks < 1) return set_err(PAC_E_ARG, "bad argument");
     c->chunk_blocks = blocks;

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void k_origin_front(PacSource src, const PacTab
     wave_spectrum_mag(dsh, T, buf, lane);
     int nm = wave_find_maskers(buf, T, 15.0, lane);
     double thr[16];
-    wave_masking(reinterpret_cast<const Masker*>(buf), nm, T, lane, thr);
+    wave_masking(buf, nm, T, lane, thr);
     wave_sync();
 
     // --- MDCT of the sine-windowed block --------------------------------
@@ -333,6 +333,38 @@ __global__ __launch_bounds__(64) void k_origin_pack(PacSource src, const PacTabl
     wave_sync();
     const int nbytes = W.nbytes[g] - 4;
     store_block_bytes(out + off[g], words, nbytes, lane);
+}
+
+// ---------------------------------------------------------------------------
+// debug / parity probe: the masking threshold of arbitrary 2048-sample blocks
+// (data already windowed as calcBTHR receives it; Hann applied here)
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restrict__ T,
+                                                        const double* __restrict__ data, int no_drop,
+                                                        double* __restrict__ thr_out,
+                                                        int32_t* __restrict__ npeaks) {
+    __shared__ double2 buf[1024];
+    const int lane = threadIdx.x;
+    const double* d = data + (int64_t)blockIdx.x * PAC_N;
+    wave_spectrum_mag([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, lane);
+    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane);
+    double thr[16];
+    wave_masking(buf, nm, T, lane, thr);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = thr[q];
+    if (lane == 0) npeaks[blockIdx.x] = nm;
+}
+
+// MDCT probe: mdct.py:49-82 of n raw (unwindowed) blocks, sine window applied
+__global__ __launch_bounds__(64) void k_debug_mdct(const PacTables* __restrict__ T,
+                                                   const double* __restrict__ data, double* __restrict__ X) {
+    __shared__ double2 buf[512];
+    __shared__ double Xs[1024];
+    const int lane = threadIdx.x;
+    const double* d = data + (int64_t)blockIdx.x * PAC_N;
+    wave_mdct([&](int i) { return __dmul_rn(d[i], T->sine[i]); }, T, buf, Xs, lane);
+    for (int k = lane; k < PAC_HALFN; k += WAVE) X[(int64_t)blockIdx.x * PAC_HALFN + k] = Xs[k];
 }
 
 // ---------------------------------------------------------------------------

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(64) void k_master_thr(PacSource src, const PacTable
     wave_spectrum_mag(d, T, buf, lane);
     int nm = wave_find_maskers(buf, T, v >= 4 ? 0.0 : 15.0, lane);
     double thr[16];
-    wave_masking(reinterpret_cast<const Masker*>(buf), nm, T, lane, thr);
+    wave_masking(buf, nm, T, lane, thr);
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[q * WAVE + lane] = thr[q];

@@ -131,18 +131,18 @@ __device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* 
 
 // Masker list in LDS, structure of arrays over the 16 KB scratch (2048 doubles):
 //   z[m]   Bark(f_m)                                       [0, 512)
-//   E[m]   10^((SPL_m - drop - 96)/10) = 2^B_m            [512, 1024)
+//   B[m]   (SPL_m - drop - 96) * log2(10)/10               [512, 1024)
 //   ku[m]  (0.367*max(SPL_m-40,0) - 27) * log2(10)/10      [1024, 1536)
-//   sfx[]  per-row suffix sums of the lower-side terms      [1536, 2048)
+//   E[m]   2^B[m] = 10^((SPL_m - drop - 96)/10)            [1536, 2048)
 // Maskers are in ascending frequency, the reference's summation order.
 #define PAC_LOG2_10_OVER_10 0.33219280948873624   // log2(10)/10
 #define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
 #define PAC_LN2 0.6931471805599453
 
 __device__ __forceinline__ double* mk_z(double2* buf) { return reinterpret_cast<double*>(buf); }
-__device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<double*>(buf) + 512; }
+__device__ __forceinline__ double* mk_B(double2* buf) { return reinterpret_cast<double*>(buf) + 512; }
 __device__ __forceinline__ double* mk_ku(double2* buf) { return reinterpret_cast<double*>(buf) + 1024; }
-__device__ __forceinline__ double* mk_sfx(double2* buf) { return reinterpret_cast<double*>(buf) + 1536; }
+__device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<double*>(buf) + 1536; }
 
 // findpeaks (psychoac.py:158-191) on |X| held in buf[k].x, masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
@@ -173,8 +173,9 @@ __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* 
     }
     wave_sync();   // all magnitude reads done before the list overwrites buf
     double* mz = mk_z(buf);
-    double* mE = mk_E(buf);
+    double* mB = mk_B(buf);
     double* mku = mk_ku(buf);
+    double* mE = mk_E(buf);
     int base = 0;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
@@ -185,9 +186,11 @@ __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* 
             double sp = S[j];
             double lev = sp - 40.0;
             lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
+            double B = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
             mz[idx] = T->bark_bin[k];
-            mE[idx] = pac_exp2((sp - drop - 96.0) * PAC_LOG2_10_OVER_10);
+            mB[idx] = B;
             mku[idx] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
+            mE[idx] = pac_exp2(B);
         }
         base += __popcll(bal[j]);
     }
@@ -200,23 +203,40 @@ __device__ __forceinline__ double pac_exp2_dd(double h, double l) {
     return pac_exp2(h) * __builtin_fma(l, PAC_LN2, 1.0);
 }
 
-// k * (a - b) as a double-double (TwoSum, then TwoProduct with an fma)
-__device__ __forceinline__ void dd_scaled_diff(double k, double a, double b, double& hi, double& lo) {
+// c + k * (a - b) as a double-double (TwoSum, TwoProduct via fma, TwoSum)
+__device__ __forceinline__ void dd_affine(double c, double k, double a, double b, double& hi, double& lo) {
     double s = a - b;
     double bb = s - a;
     double err = (a - (s - bb)) + (-b - bb);
-    hi = k * s;
-    lo = __builtin_fma(k, s, -hi) + k * err;
+    double ph = k * s;
+    double pl = __builtin_fma(k, s, -ph) + k * err;
+    double t = c + ph;
+    double cc = t - c;
+    double e2 = (c - (t - cc)) + (ph - cc);
+    hi = t;
+    lo = e2 + pl;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w < v ? w : v; }
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w > v ? w : v; }
+    return v;
 }
 
 // Masking threshold (psychoac.py:447-456): for each MDCT line
 //   I(l) = sum_m 10^((spl_m(l) - 96)/10) + Intensity(Thresh(f_l)),  thr = SPL(I)
 // with spl_m(l) = SPL_m + spread(dz) - drop, dz = Bark(f_l) - Bark(f_m).
 // The sum splits by dz (the reference's slope selection, psychoac.py:111-116):
-//   dz >  1/2 (masker below the line): E_m 2^(ku_m (dz - 1/2))   per-pair exp2,
-//              skipped when below 2^-64 of a lower bound of the line's total;
-//   |dz| <= 1/2 (flat):                E_m                       no exp;
-//   dz < -1/2 (masker above the line): E_m 2^(KL (z_m - 1/2 - z_r)) * 2^(KL (z_r - z_l))
+//   dz >  1/2 (masker below the line): 2^(B_m + ku_m (dz - 1/2))   per-pair exp2;
+//              a leading run of maskers whose largest term over the row is
+//              below 2^-64 of a lower bound of every line's total is skipped;
+//   |dz| <= 1/2 (flat):                E_m = 2^B_m                no exp;
+//   dz < -1/2 (masker above the line): 2^(B_m + KL (z_m - 1/2 - z_r)) * 2^(KL (z_r - z_l))
 //              -- the lower slope is the constant -27 dB/Bark, so these terms
 //              factor into per-row suffix sums over maskers (one exp2 per
 //              masker per row instead of per line), exponents in double-double.
@@ -225,14 +245,14 @@ __device__ __forceinline__ void dd_scaled_diff(double k, double a, double b, dou
 __device__ __forceinline__ void wave_masking(double2* buf, int nm, const PacTables* __restrict__ T,
                                              int lane, double thr[16]) {
     const double* mz = mk_z(buf);
-    const double* mE = mk_E(buf);
+    const double* mB = mk_B(buf);
     const double* mku = mk_ku(buf);
-    double* sfx = mk_sfx(buf);
+    const double* mE = mk_E(buf);
 #pragma unroll 1
     for (int r = 0; r < 16; ++r) {
         const int l = r * WAVE + lane;
         const double zl = T->bark_line[l];
-        const double zr = T->bark_line[r * WAVE];          // row reference (smallest z)
+        const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
         // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending)
         int lo = 0, hi = nm;
         while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] > 0.5) lo = mid + 1; else hi = mid; }
@@ -240,70 +260,63 @@ __device__ __forceinline__ void wave_masking(double2* buf, int nm, const PacTabl
         hi = nm;
         while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] >= -0.5) lo = mid + 1; else hi = mid; }
         const int V = lo;
-        // --- lower side: suffix sums of P_m = E_m 2^(KL (z_m - 1/2 - zr)) over m >= Vmin
-        int vmin = V;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(vmin, o, WAVE); vmin = w < vmin ? w : vmin; }
-        double carry = 0.0;
+        // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
+        //     gathered at each lane's V by a cross-lane shuffle (no LDS)
+        const int vmin = wave_min_i(V);
+        double carry = 0.0, sv = 0.0;
         for (int top = nm; top > vmin; top -= WAVE) {
             const int m = top - WAVE + lane;
             double x = 0.0;
             if (m >= vmin) {
                 double h, lo2;
-                dd_scaled_diff(PAC_KL, mz[m] - 0.5, zr, h, lo2);
-                x = mE[m] * pac_exp2_dd(h, lo2);
+                dd_affine(mB[m], PAC_KL, mz[m] - 0.5, zr, h, lo2);
+                x = pac_exp2_dd(h, lo2);
             }
-            // inclusive suffix scan inside the 64-wide chunk
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
+            for (int o = 1; o < 64; o <<= 1) {            // inclusive suffix scan in the chunk
                 double y = __shfl_down(x, o, WAVE);
                 if (lane + o < 64) x += y;
             }
             const double tot = __shfl(x, 0, WAVE);
-            if (m >= vmin) sfx[m] = x + carry;
+            const int idx = V - (top - WAVE);
+            const double g = __shfl(x, idx & 63, WAVE) + carry;
+            if (idx >= 0 && idx < WAVE) sv = g;
             carry += tot;
         }
-        wave_sync();
         double lower = 0.0;
         if (V < nm) {
             double h, lo2;
-            dd_scaled_diff(-PAC_KL, zl, zr, h, lo2);
-            lower = sfx[V] * pac_exp2_dd(h, lo2);
+            dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
+            lower = sv * pac_exp2_dd(h, lo2);
         }
         // --- flat zone, ascending
         double flat = 0.0;
-        int umin = U, vmax = V;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            int w = __shfl_xor(umin, o, WAVE); umin = w < umin ? w : umin;
-            int x2 = __shfl_xor(vmax, o, WAVE); vmax = x2 > vmax ? x2 : vmax;
-        }
+        const int umin = wave_min_i(U), vmax = wave_max_i(V);
         for (int m = umin; m < vmax; ++m) {
             double e = mE[m];
             if (m >= U && m < V) flat += e;
         }
-        // --- upper side, ascending, with negligible-term skipping
+        // --- upper side, ascending
         const double tiq = T->tiq[l];
         double lb = tiq + flat + lower;                       // I(l) >= lb
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
-        const double cut = lb * 0x1.0p-64;
-        int umax = U;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(umax, o, WAVE); umax = w > umax ? w : umax; }
-        const double z0 = zr;                                 // smallest line z of the row
+        const double l2cut = log2(lb) - 64.0;
+        const int umax = wave_max_i(U);
+        int m0 = 0;
+        for (; m0 < umax; ++m0) {         // leading negligible maskers (wave-uniform test)
+            const double ku = mku[m0];
+            const double t = __builtin_fma(fmax((zr - mz[m0]) - 0.5, 0.0), ku, mB[m0]);
+            const int keep = !(ku < 0.0 && t < l2cut);
+            if (__builtin_amdgcn_readfirstlane(keep)) break;
+        }
         double up = 0.0;
 #pragma unroll 2
-        for (int m = 0; m < umax; ++m) {
-            const double zm = mz[m], E = mE[m], ku = mku[m];
-            // largest term of this masker over the row (ku < 0: at the lowest line)
-            double a0 = fmax((z0 - zm) - 0.5, 0.0);
-            if (ku < 0.0 && E * pac_exp2(ku * a0) < cut) continue;   // wave-uniform
-            double a = (zl - zm) - 0.5;
-            double t = E * pac_exp2(ku * a);
+        for (int m = m0; m < umax; ++m) {
+            const double a = (zl - mz[m]) - 0.5;
+            const double t = pac_exp2(__builtin_fma(a, mku[m], mB[m]));
             up += (m < U) ? t : 0.0;
         }
         thr[r] = pac_spl(((up + flat) + lower) + tiq);
-        wave_sync();   // this row's sfx reads precede the next row's writes
     }
 }

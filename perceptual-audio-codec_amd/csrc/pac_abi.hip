@@ -191,6 +191,7 @@ struct pac_ctx {
     PacHuffTables* huff_host = nullptr;
     std::unordered_map<uint64_t, int> huff_dec[PAC_NTAB];   // (len<<32|code) -> symbol, -1 = escape
     int64_t chunk_blocks = 32768;
+    int dbg = 0;                           // PAC_DEBUG_FLAGS (diagnostic builds of the timing only)
     // timing
     bool timing = false;
     hipEvent_t ev[5] = {};
@@ -210,6 +211,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
     }
     for (auto& e : c->ev) hipEventCreate(&e);
+    if (const char* f = getenv("PAC_DEBUG_FLAGS")) c->dbg = atoi(f);
     *out = c;
     return PAC_OK;
 }
@@ -546,7 +548,7 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         if ((rc = c->out_stage.ensure(want))) return rc;
         out_dev = c->out_stage.p;
     }
-    PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch};
+    PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch, c->dbg};
     int64_t total = 0;
     if (master) {
         if ((rc = c->st_extra.ensure(n_streams)) || (rc = c->st_deposit.ensure(n_streams))) return rc;
@@ -624,7 +626,7 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
         (rc = c->blk_off.ensure(2)) || (rc = c->stream_off.ensure(2)))
         return rc;
     HIPCHK(hipMemcpyAsync(c->fsrc.p, full_block, G * PAC_N * sizeof(double), hipMemcpyHostToDevice, s));
-    PacSource src{nullptr, nullptr, c->blk_off.p, c->fsrc.p, 1, nch};
+    PacSource src{nullptr, nullptr, c->blk_off.p, c->fsrc.p, 1, nch, 0};
     int64_t total = 0;
     std::vector<double> smr(PAC_NB * G);
     int32_t lrms[PAC_NB] = {0};

@@ -10,6 +10,7 @@ struct PacSource {
     const double* fsrc;        // OR float64 blocks [n_blocks][n_ch][2048] (device), per-block API
     int n_streams;
     int n_ch;
+    int dbg;                   // diagnostic phase switches (PAC_DEBUG_FLAGS), 0 in production
 };
 
 // Per-channel-block work arrays (structure of arrays: index [band * G + g]).

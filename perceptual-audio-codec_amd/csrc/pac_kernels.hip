@@ -83,6 +83,7 @@ __global__ __launch_bounds__(64) void k_origin_front(PacSource src, const PacTab
     wave_spectrum_mag(dsh, T, buf, lane);
     int nm = wave_find_maskers(buf, T, 15.0, lane);
     double thr[16];
+    if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     wave_masking(buf, nm, T, lane, thr);
     wave_sync();
 

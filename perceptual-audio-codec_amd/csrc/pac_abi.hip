@@ -370,7 +370,7 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     PacOriginWork W{c->smr.p, c->bandpeak.p, c->overall.p, c->ba.p, c->sf.p, c->nbytes.p};
     hipStream_t s = c->stream;
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(64), 0, s, src, T, W, G);
+    hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_origin_alloc, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, T, W, G,
@@ -389,7 +389,7 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     HIPCHK(hipStreamSynchronize(s));
     if (total > out_cap) return set_err(PAC_E_CAPACITY, "output needs %lld bytes, capacity %lld",
                                         (long long)total, (long long)out_cap);
-    hipLaunchKernelGGL(k_origin_pack, dim3((unsigned)G), dim3(64), 0, s, src, T, W, G, c->off.p, out_dev);
+    hipLaunchKernelGGL(k_origin_pack, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G, c->off.p, out_dev);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[4], s));
     *out_total = total;
@@ -443,7 +443,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         int s_first = (int)(std::upper_bound(blk.begin(), blk.end(), gb0) - blk.begin()) - 1;
         int s_last = (int)(std::upper_bound(blk.begin(), blk.end(), gb1 - 1) - blk.begin()) - 1;
         if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
-        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(64), 0, s, src, T, W, gb0);
+        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, gb0);
         hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(64), 0, s, src, T, W, gb0);
         HIPCHK(hipGetLastError());
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));

@@ -71,54 +71,72 @@ __device__ __forceinline__ double sample(const BlockRef& r, int i) {
 // origin front: MDCT, overall scale, threshold, SMR
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(64) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
-                                                     PacOriginWork W, int64_t G) {
+#define FRONT_NT 256
+
+__device__ __forceinline__ double block_max_256(double v, double* red) {
+    v = wave_max(v);
+    if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    double r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    return r;
+}
+
+// One 256-thread workgroup per channel-block: the FFTs are shared by the four
+// waves; each wave sweeps the masking sum for rows w, w+4, w+8, w+12.
+__global__ __launch_bounds__(FRONT_NT) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
+                                                           PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: spectrum / masker list / MDCT scratch
-    const int lane = threadIdx.x;
+    __shared__ int cnt[16];
+    __shared__ double red[4];
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int w = tid / WAVE;
     const int64_t g = blockIdx.x;
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
 
     // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
     auto dsh = [&](int i) { return __dmul_rn(__dmul_rn(sample(r, i), T->sine[i]), T->hann[i]); };
-    wave_spectrum_mag(dsh, T, buf, lane);
-    int nm = wave_find_maskers(buf, T, 15.0, lane);
-    double thr[16];
+    grp_spectrum_mag<FRONT_NT>(dsh, T, buf, tid);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
-    wave_masking(buf, nm, T, lane, thr);
-    wave_sync();
+    double thr[4];
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) thr[i] = wave_masking_row(buf, nm, T, lane, w + 4 * i);
+    __syncthreads();
 
     // --- MDCT of the sine-windowed block --------------------------------
     double* X = reinterpret_cast<double*>(buf + 512);
     auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
-    wave_mdct(xs, T, buf, X, lane);
+    grp_mdct<FRONT_NT>(xs, T, buf, X, tid);
     double mx = 0.0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) mx = fmax(mx, fabs(X[j * WAVE + lane]));
-    mx = wave_max(mx);
+    for (int j = 0; j < 4; ++j) mx = fmax(mx, fabs(X[j * FRONT_NT + tid]));
+    mx = block_max_256(mx, red);
     const int overall = pac_scale_factor(mx, 5);
     const double gain = (double)(1 << overall);
 
     // --- SMR (Origin psychoac.py:281-314): SPL(4 (X/2^s)^2) - thr ---------
     double* d = reinterpret_cast<double*>(buf);     // 1024 doubles (first 8 KB)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        int l = j * WAVE + lane;
+    for (int i = 0; i < 4; ++i) {
+        int l = (w + 4 * i) * WAVE + lane;
         double x = X[l];                        // unscaled; (x*2^s)/2^s == x exactly
-        d[l] = pac_spl(4.0 * (x * x)) - thr[j];
+        d[l] = pac_spl(4.0 * (x * x)) - thr[i];
     }
-    wave_sync();
+    __syncthreads();
     // band peak |line| of the SCALED lines, for the scale factors
-    if (lane < PAC_NB) {
-        int lo = T->lower[lane], n = T->nlines[lane];
+    if (tid < PAC_NB) {
+        int lo = T->lower[tid], n = T->nlines[tid];
         double sm = -INFINITY, pk = 0.0;
         for (int l = lo; l < lo + n; ++l) {
             sm = fmax(sm, d[l]);
             pk = fmax(pk, fabs(X[l] * gain));
         }
-        W.smr[lane * G + g] = n ? sm : 0.0;
-        W.bandpeak[lane * G + g] = pk;
+        W.smr[tid * G + g] = n ? sm : 0.0;
+        W.bandpeak[tid * G + g] = pk;
     }
-    if (lane == 0) W.overall[g] = (uint8_t)overall;
+    if (tid == 0) W.overall[g] = (uint8_t)overall;
 }
 
 // ---------------------------------------------------------------------------
@@ -289,41 +307,41 @@ __device__ __forceinline__ void store_block_bytes(uint8_t* __restrict__ out, con
 // origin pack: one wave per channel-block
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(64) void k_origin_pack(PacSource src, const PacTables* __restrict__ T,
-                                                    PacOriginWork W, int64_t G,
-                                                    const int64_t* __restrict__ off,
-                                                    uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const PacTables* __restrict__ T,
+                                                          PacOriginWork W, int64_t G,
+                                                          const int64_t* __restrict__ off,
+                                                          uint8_t* __restrict__ out) {
     __shared__ double2 buf[512];
     __shared__ double X[1024];
     __shared__ uint32_t words[PACK_WORDS];
     __shared__ int start[PAC_NB];
     __shared__ int bas[PAC_NB], sfs[PAC_NB];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
     const int64_t g = blockIdx.x;
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
-    for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
-    if (lane < PAC_NB) {
-        bas[lane] = W.ba[lane * G + g];
-        sfs[lane] = W.sf[lane * G + g];
+    for (int i = tid; i < PACK_WORDS; i += FRONT_NT) words[i] = 0;
+    if (tid < PAC_NB) {
+        bas[tid] = W.ba[tid * G + g];
+        sfs[tid] = W.sf[tid * G + g];
     }
     auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
-    wave_mdct(xs, T, buf, X, lane);      // identical to the front kernel's lines
-    if (lane == 0) {
+    grp_mdct<FRONT_NT>(xs, T, buf, X, tid);      // identical to the front kernel's lines
+    if (tid == 0) {
         int p = 4;
         for (int b = 0; b < PAC_NB; ++b) { start[b] = p; p += 8 + bas[b] * T->nlines[b]; }
     }
-    wave_sync();
+    __syncthreads();
     const int overall = W.overall[g];
     const double gain = (double)(1 << overall);
-    if (lane == 0) put_bits(words, 0, (uint32_t)overall, 4);
-    if (lane < PAC_NB) {
-        int ba = bas[lane];
-        put_bits(words, start[lane], (uint32_t)(ba ? ba - 1 : 0), 4);
-        put_bits(words, start[lane] + 4, (uint32_t)sfs[lane], 4);
+    if (tid == 0) put_bits(words, 0, (uint32_t)overall, 4);
+    if (tid < PAC_NB) {
+        int ba = bas[tid];
+        put_bits(words, start[tid], (uint32_t)(ba ? ba - 1 : 0), 4);
+        put_bits(words, start[tid] + 4, (uint32_t)sfs[tid], 4);
     }
-#pragma unroll 4
-    for (int j = 0; j < 16; ++j) {
-        int l = j * WAVE + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int l = j * FRONT_NT + tid;
         int b = T->band_of_line[l];
         int ba = bas[b];
         if (ba) {
@@ -331,9 +349,11 @@ __global__ __launch_bounds__(64) void k_origin_pack(PacSource src, const PacTabl
             put_bits(words, start[b] + 8 + (l - T->lower[b]) * ba, m, ba);
         }
     }
-    wave_sync();
+    __syncthreads();
     const int nbytes = W.nbytes[g] - 4;
-    store_block_bytes(out + off[g], words, nbytes, lane);
+    uint8_t* o = out + off[g];
+    if (tid < 4) o[tid] = (uint8_t)((uint32_t)nbytes >> (8 * tid));   // '<L' nBytes
+    for (int i = tid; i < nbytes; i += FRONT_NT) o[4 + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
 }
 
 // ---------------------------------------------------------------------------

@@ -44,22 +44,26 @@ __device__ __forceinline__ double variant_sample(const BlockRef& rL, const Block
     return ms;
 }
 
-__global__ __launch_bounds__(64) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                   PacMasterWork W, int64_t gb0) {
+__global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
+                                                         PacMasterWork W, int64_t gb0) {
     __shared__ double2 buf[1024];
-    const int lane = threadIdx.x;
+    __shared__ int cnt[16];
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int w = tid / WAVE;
     const int64_t j = blockIdx.x / 6;          // block within the chunk
     const int v = blockIdx.x % 6;
     const BlockRef rL = locate(src, gb0 + j, 0);
     const BlockRef rR = locate(src, gb0 + j, 1);
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
-    wave_spectrum_mag(d, T, buf, lane);
-    int nm = wave_find_maskers(buf, T, v >= 4 ? 0.0 : 15.0, lane);
-    double thr[16];
-    wave_masking(buf, nm, T, lane, thr);
+    grp_spectrum_mag<FRONT_NT>(d, T, buf, tid);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, cnt);
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) out[q * WAVE + lane] = thr[q];
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        int r = w + 4 * i;
+        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r);
+    }
 }
 
 // --- numpy pairwise summation of a complex vector (loops_utils.h.src) -------

@@ -33,19 +33,25 @@ __device__ __forceinline__ unsigned brev(unsigned x, int bits) {
     return __builtin_bitreverse32(x) >> (32 - bits);
 }
 
+template <int NT>
+__device__ __forceinline__ void grp_sync() {
+    if constexpr (NT == WAVE) wave_sync(); else __syncthreads();
+}
+
 // In-place radix-2 DIT FFT of n = 2^LOG complex values that were stored in
-// bit-reversed order.  Twiddles: tw[k] = exp(-2 pi i k / 1024), k < 512.
-template <int LOG>
-__device__ __forceinline__ void wave_fft(double2* buf, const double2* __restrict__ tw, int lane) {
+// bit-reversed order, by a group of NT threads (one wave or a workgroup).
+// Twiddles: tw[k] = exp(-2 pi i k / 1024), k < 512.
+template <int LOG, int NT>
+__device__ __forceinline__ void grp_fft(double2* buf, const double2* __restrict__ tw, int tid) {
     constexpr int n = 1 << LOG;
 #pragma unroll 1
     for (int s = 1; s <= LOG; ++s) {
         const int half = 1 << (s - 1);
         const int tstride = 1024 >> s;
-        wave_sync();
+        grp_sync<NT>();
 #pragma unroll
-        for (int t0 = 0; t0 < n / 2; t0 += WAVE) {
-            int t = t0 + lane;
+        for (int t0 = 0; t0 < n / 2; t0 += NT) {
+            int t = t0 + tid;
             int k = t & (half - 1);
             int i = ((t >> (s - 1)) << s) + k;
             double2 w = tw[k * tstride];
@@ -55,20 +61,20 @@ __device__ __forceinline__ void wave_fft(double2* buf, const double2* __restrict
             buf[i + half] = make_double2(__dsub_rn(a.x, bw.x), __dsub_rn(a.y, bw.y));
         }
     }
-    wave_sync();
+    grp_sync<NT>();
 }
 
 // MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
 // sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
 // place in codec.py:240).  Evaluated as DCT-IV of the folded block with a
 // 512-point complex FFT.  buf: 512 double2 of LDS scratch.  Output: X[1024]
-// in LDS.
-template <class XS>
-__device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restrict__ T,
-                                          double2* buf, double* X, int lane) {
+// in LDS.  An exactly-zero line keeps the reference's sign (mdct_zero_neg).
+template <int NT, class XS>
+__device__ __forceinline__ void grp_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                         double2* buf, double* X, int tid) {
 #pragma unroll
-    for (int q0 = 0; q0 < 512; q0 += WAVE) {
-        int q = q0 + lane;
+    for (int q0 = 0; q0 < 512; q0 += NT) {
+        int q = q0 + tid;
         int n0 = 2 * q, n1 = 1023 - 2 * q;
         // fold [a b c d] -> (-c_r - d, a - b_r)
         double u0 = n0 < 512 ? __dsub_rn(-xs(1535 - n0), xs(1536 + n0))
@@ -77,10 +83,10 @@ __device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restr
                              : __dsub_rn(xs(n1 - 512), xs(1535 - n1));
         buf[brev(q, 9)] = cmul(make_double2(u0, u1), T->mdct_pre[q]);
     }
-    wave_fft<9>(buf, T->fft_tw, lane);
+    grp_fft<9, NT>(buf, T->fft_tw, tid);
 #pragma unroll
-    for (int q0 = 0; q0 < 512; q0 += WAVE) {
-        int q = q0 + lane;
+    for (int q0 = 0; q0 < 512; q0 += NT) {
+        int q = q0 + tid;
         double2 y = cmul(buf[q], T->mdct_post[q]);
         double x0 = y.x * (1.0 / 1024.0), x1 = -y.y * (1.0 / 1024.0);
         if (x0 == 0.0) x0 = T->mdct_zero_neg[2 * q] ? -0.0 : 0.0;
@@ -88,24 +94,24 @@ __device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restr
         X[2 * q] = x0;
         X[1023 - 2 * q] = x1;
     }
-    wave_sync();
+    grp_sync<NT>();
 }
 
 // |FFT(d)[k]|, k < 1024, of a real 2048-sample block d(i) via a 1024-point
 // complex FFT.  buf: 1024 double2 of LDS; on return buf[k].x = |X[k]|.
-template <class DS>
-__device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
-                                                  double2* buf, int lane) {
+template <int NT, class DS>
+__device__ __forceinline__ void grp_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
+                                                 double2* buf, int tid) {
 #pragma unroll 4
-    for (int n0 = 0; n0 < 1024; n0 += WAVE) {
-        int n = n0 + lane;
+    for (int n0 = 0; n0 < 1024; n0 += NT) {
+        int n = n0 + tid;
         buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
     }
-    wave_fft<10>(buf, T->fft_tw, lane);
+    grp_fft<10, NT>(buf, T->fft_tw, tid);
     // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k])
 #pragma unroll
-    for (int t0 = 0; t0 <= 512; t0 += WAVE) {
-        int k = t0 + lane;
+    for (int t0 = 0; t0 <= 512; t0 += NT) {
+        int k = t0 + tid;
         if (k > 512) continue;
         int k2 = (1024 - k) & 1023;
         double2 Za = buf[k], Zb = buf[k2];
@@ -117,7 +123,6 @@ __device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* 
             double2 Bc = side ? Za : Zb;  // Z[M-kk]
             double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
             double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
-            // -i * W^kk * o
             double2 wo = cmul(T->rfft_tw[kk], o);
             double xr = e.x + wo.y;
             double xi = e.y - wo.x;
@@ -126,7 +131,23 @@ __device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* 
         buf[k].x = mags[0];
         if (k2 != k) buf[k2].x = mags[1];
     }
-    wave_sync();
+    grp_sync<NT>();
+}
+
+// one-wave aliases used by the single-wave kernels
+template <int LOG>
+__device__ __forceinline__ void wave_fft(double2* buf, const double2* __restrict__ tw, int lane) {
+    grp_fft<LOG, WAVE>(buf, tw, lane);
+}
+template <class XS>
+__device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                          double2* buf, double* X, int lane) {
+    grp_mdct<WAVE>(xs, T, buf, X, lane);
+}
+template <class DS>
+__device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
+                                                  double2* buf, int lane) {
+    grp_spectrum_mag<WAVE>(d, T, buf, lane);
 }
 
 // Masker list in LDS, structure of arrays over the 16 KB scratch (2048 doubles):
@@ -146,15 +167,20 @@ __device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<
 
 // findpeaks (psychoac.py:158-191) on |X| held in buf[k].x, masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
-// compacted masker list written over buf.  Returns the masker count.
-__device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                 double drop, int lane) {
+// compacted masker list (ascending bin order) written over buf by a group of
+// NT threads.  cnt: LDS scratch of (1024/WAVE) ints.  Returns the masker count.
+template <int NT>
+__device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T,
+                                                double drop, int tid, int* cnt) {
+    constexpr int J = 1024 / NT;
+    const int lane = tid & (WAVE - 1);
+    const int w = tid / WAVE;
     const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
-    double S[16];
-    unsigned long long bal[16];
+    double S[J];
+    unsigned long long bal[J];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        int k = j * WAVE + lane;
+    for (int j = 0; j < J; ++j) {
+        int k = j * NT + tid;
         bool pk = false;
         S[j] = 0.0;
         if (k >= 1 && k <= 1022) {
@@ -170,19 +196,24 @@ __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* 
             S[j] = pac_spl(csp * s);
         }
         bal[j] = __ballot(pk);
+        if (lane == 0) cnt[j * (NT / WAVE) + w] = __popcll(bal[j]);   // segment (j, w) in bin order
     }
-    wave_sync();   // all magnitude reads done before the list overwrites buf
+    grp_sync<NT>();   // all magnitude reads and counts done before the list overwrites buf
+    int tot = 0;
+    for (int i = 0; i < 1024 / WAVE; ++i) tot += cnt[i];
     double* mz = mk_z(buf);
     double* mB = mk_B(buf);
     double* mku = mk_ku(buf);
     double* mE = mk_E(buf);
-    int base = 0;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < J; ++j) {
         if ((bal[j] >> lane) & 1ull) {
+            int base = 0;
+            const int seg = j * (NT / WAVE) + w;
+            for (int i = 0; i < seg; ++i) base += cnt[i];
             int idx = base + __popcll(bal[j] & below);
-            int k = j * WAVE + lane;
+            int k = j * NT + tid;
             double sp = S[j];
             double lev = sp - 40.0;
             lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
@@ -192,10 +223,15 @@ __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* 
             mku[idx] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
             mE[idx] = pac_exp2(B);
         }
-        base += __popcll(bal[j]);
     }
-    wave_sync();
-    return base;
+    grp_sync<NT>();
+    return tot;
+}
+
+__device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
+                                                 double drop, int lane) {
+    __shared__ int cnt_w[1024 / WAVE];
+    return grp_find_maskers<WAVE>(buf, T, drop, lane, cnt_w);
 }
 
 // 2^(h + l) for a double-double exponent (|l| << ulp(h)): exp2(h) * (1 + l ln2)
@@ -242,81 +278,85 @@ __device__ __forceinline__ int wave_max_i(int v) {
 //              masker per row instead of per line), exponents in double-double.
 // Values agree with the direct ascending sum to ~1e-15 relative.  Lane owns
 // lines l = 64 r + lane, rows r = 0..15.
-__device__ __forceinline__ void wave_masking(double2* buf, int nm, const PacTables* __restrict__ T,
-                                             int lane, double thr[16]) {
+__device__ __forceinline__ double wave_masking_row(double2* buf, int nm, const PacTables* __restrict__ T,
+                                                   int lane, int r) {
     const double* mz = mk_z(buf);
     const double* mB = mk_B(buf);
     const double* mku = mk_ku(buf);
     const double* mE = mk_E(buf);
-#pragma unroll 1
-    for (int r = 0; r < 16; ++r) {
-        const int l = r * WAVE + lane;
-        const double zl = T->bark_line[l];
-        const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
-        // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending)
-        int lo = 0, hi = nm;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] > 0.5) lo = mid + 1; else hi = mid; }
-        const int U = lo;
-        hi = nm;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] >= -0.5) lo = mid + 1; else hi = mid; }
-        const int V = lo;
-        // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
-        //     gathered at each lane's V by a cross-lane shuffle (no LDS)
-        const int vmin = wave_min_i(V);
-        double carry = 0.0, sv = 0.0;
-        for (int top = nm; top > vmin; top -= WAVE) {
-            const int m = top - WAVE + lane;
-            double x = 0.0;
-            if (m >= vmin) {
-                double h, lo2;
-                dd_affine(mB[m], PAC_KL, mz[m] - 0.5, zr, h, lo2);
-                x = pac_exp2_dd(h, lo2);
-            }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {            // inclusive suffix scan in the chunk
-                double y = __shfl_down(x, o, WAVE);
-                if (lane + o < 64) x += y;
-            }
-            const double tot = __shfl(x, 0, WAVE);
-            const int idx = V - (top - WAVE);
-            const double g = __shfl(x, idx & 63, WAVE) + carry;
-            if (idx >= 0 && idx < WAVE) sv = g;
-            carry += tot;
-        }
-        double lower = 0.0;
-        if (V < nm) {
+    const int l = r * WAVE + lane;
+    const double zl = T->bark_line[l];
+    const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
+    // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending)
+    int lo = 0, hi = nm;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] > 0.5) lo = mid + 1; else hi = mid; }
+    const int U = lo;
+    hi = nm;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] >= -0.5) lo = mid + 1; else hi = mid; }
+    const int V = lo;
+    // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
+    //     gathered at each lane's V by a cross-lane shuffle (no LDS)
+    const int vmin = wave_min_i(V);
+    double carry = 0.0, sv = 0.0;
+    for (int top = nm; top > vmin; top -= WAVE) {
+        const int m = top - WAVE + lane;
+        double x = 0.0;
+        if (m >= vmin) {
             double h, lo2;
-            dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
-            lower = sv * pac_exp2_dd(h, lo2);
+            dd_affine(mB[m], PAC_KL, mz[m] - 0.5, zr, h, lo2);
+            x = pac_exp2_dd(h, lo2);
         }
-        // --- flat zone, ascending
-        double flat = 0.0;
-        const int umin = wave_min_i(U), vmax = wave_max_i(V);
-        for (int m = umin; m < vmax; ++m) {
-            double e = mE[m];
-            if (m >= U && m < V) flat += e;
-        }
-        // --- upper side, ascending
-        const double tiq = T->tiq[l];
-        double lb = tiq + flat + lower;                       // I(l) >= lb
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
-        const double l2cut = log2(lb) - 64.0;
-        const int umax = wave_max_i(U);
-        int m0 = 0;
-        for (; m0 < umax; ++m0) {         // leading negligible maskers (wave-uniform test)
-            const double ku = mku[m0];
-            const double t = __builtin_fma(fmax((zr - mz[m0]) - 0.5, 0.0), ku, mB[m0]);
-            const int keep = !(ku < 0.0 && t < l2cut);
-            if (__builtin_amdgcn_readfirstlane(keep)) break;
+        for (int o = 1; o < 64; o <<= 1) {            // inclusive suffix scan in the chunk
+            double y = __shfl_down(x, o, WAVE);
+            if (lane + o < 64) x += y;
         }
-        double up = 0.0;
-#pragma unroll 2
-        for (int m = m0; m < umax; ++m) {
-            const double a = (zl - mz[m]) - 0.5;
-            const double t = pac_exp2(__builtin_fma(a, mku[m], mB[m]));
-            up += (m < U) ? t : 0.0;
-        }
-        thr[r] = pac_spl(((up + flat) + lower) + tiq);
+        const double tot = __shfl(x, 0, WAVE);
+        const int idx = V - (top - WAVE);
+        const double g = __shfl(x, idx & 63, WAVE) + carry;
+        if (idx >= 0 && idx < WAVE) sv = g;
+        carry += tot;
     }
+    double lower = 0.0;
+    if (V < nm) {
+        double h, lo2;
+        dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
+        lower = sv * pac_exp2_dd(h, lo2);
+    }
+    // --- flat zone, ascending
+    double flat = 0.0;
+    const int umin = wave_min_i(U), vmax = wave_max_i(V);
+    for (int m = umin; m < vmax; ++m) {
+        double e = mE[m];
+        if (m >= U && m < V) flat += e;
+    }
+    // --- upper side, ascending
+    const double tiq = T->tiq[l];
+    double lb = tiq + flat + lower;                       // I(l) >= lb
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
+    const double l2cut = log2(lb) - 64.0;
+    const int umax = wave_max_i(U);
+    int m0 = 0;
+    for (; m0 < umax; ++m0) {         // leading negligible maskers (wave-uniform test)
+        const double ku = mku[m0];
+        const double t = __builtin_fma(fmax((zr - mz[m0]) - 0.5, 0.0), ku, mB[m0]);
+        const int keep = !(ku < 0.0 && t < l2cut);
+        if (__builtin_amdgcn_readfirstlane(keep)) break;
+    }
+    double up = 0.0;
+#pragma unroll 4
+    for (int m = m0; m < umax; ++m) {
+        const double a = (zl - mz[m]) - 0.5;
+        const double t = pac_exp2(__builtin_fma(a, mku[m], mB[m]));
+        up += (m < U) ? t : 0.0;
+    }
+    return pac_spl(((up + flat) + lower) + tiq);
+}
+
+// all 16 rows by one wave
+__device__ __forceinline__ void wave_masking(double2* buf, int nm, const PacTables* __restrict__ T,
+                                             int lane, double thr[16]) {
+#pragma unroll 1
+    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r);
 }

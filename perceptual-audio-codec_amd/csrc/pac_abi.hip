@@ -122,6 +122,12 @@ static void build_tables(int fs, PacTables* t) {
             t->mdct_zero_neg[k] = (cos(ph) < 0.0 && sin(ph) >= 0.0) ? 1 : 0;
         }
     }
+    {   // findpeaks floor: largest m with 10*log10(m) <= -30, squared
+        double m = 1e-3;
+        while (10.0 * log10(m) > -30.0) m = nextafter(m, 0.0);
+        while (10.0 * log10(nextafter(m, 1.0)) <= -30.0) m = nextafter(m, 1.0);
+        t->peak_floor2 = m * m;
+    }
     const int step = fs / PAC_N;  // Py2 integer division, psychoac.py:188
     double mx = -1.0;
     for (int k = 0; k < PAC_HALFN; k++) {

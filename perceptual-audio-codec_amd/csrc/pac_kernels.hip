@@ -67,6 +67,42 @@ __device__ __forceinline__ double sample(const BlockRef& r, int i) {
     return pac_pcm_to_float(r.pcm[f * r.nch + r.c]);
 }
 
+// The same samples with the stream-edge test hoisted: samples [ilo, ihi) of
+// the block lie inside the stream; p points at sample ilo of channel c.
+struct BlockPcm {
+    const int16_t* p;
+    const double* f;
+    int ilo, ihi, nch;
+    __device__ __forceinline__ explicit BlockPcm(const BlockRef& r) {
+        f = r.fsrc;
+        nch = r.nch;
+        if (f) { p = nullptr; ilo = 0; ihi = PAC_N; return; }
+        const int64_t ff = r.first_frame;
+        ilo = ff < 0 ? (int)(-ff) : 0;
+        const int64_t top = r.n_frames - ff;
+        ihi = top < ilo ? ilo : (top > PAC_N ? PAC_N : (int)top);
+        p = r.pcm + ((ff + ilo) * r.nch + r.c);
+    }
+    __device__ __forceinline__ double operator()(int i) const {
+        if (f) return f[i];
+        int c = 0;
+        if (i >= ilo && i < ihi) c = p[(i - ilo) * nch];
+        return pac_pcm_to_float(c);
+    }
+};
+
+// xs[i] = x(i) * sine[i] (window.py:27-39, codec.py:240) into LDS, i < 2048
+template <int NT>
+__device__ __forceinline__ void grp_stage_sine(const BlockRef& r, const PacTables* __restrict__ T,
+                                               double* xs, int tid) {
+    const BlockPcm x(r);
+#pragma unroll
+    for (int i0 = 0; i0 < PAC_N; i0 += NT) {
+        const int i = i0 + tid;
+        xs[i] = __dmul_rn(x(i), T->sine[i]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // origin front: MDCT, overall scale, threshold, SMR
 // ---------------------------------------------------------------------------
@@ -82,11 +118,28 @@ __device__ __forceinline__ double block_max_256(double v, double* red) {
     return r;
 }
 
-// One 256-thread workgroup per channel-block: the FFTs are shared by the four
-// waves; each wave sweeps the masking sum for rows w, w+4, w+8, w+12.
+// max over the lines of each band (bands b = w, w+4, ... for wave w) of v[l];
+// -inf for an empty band
+__device__ __forceinline__ void grp_band_max(const PacTables* __restrict__ T, const double* v, int w,
+                                             int lane, double* out, int64_t stride, double scale,
+                                             bool empty_zero) {
+    for (int b = w; b < PAC_NB; b += FRONT_NT / WAVE) {
+        const int lo = T->lower[b], n = T->nlines[b];
+        double m = -INFINITY;
+        for (int l = lo + lane; l < lo + n; l += WAVE) m = fmax(m, v[l]);
+        m = wave_max(m);
+        if (lane == 0) out[b * stride] = (n == 0 && empty_zero) ? 0.0 : m * scale;
+    }
+}
+
+// One 256-thread workgroup per channel-block.  The block is windowed once
+// into LDS; the MDCT runs first (lines kept in registers, band peaks taken),
+// then the Hann spectrum whose masker list the four waves share; each wave
+// sweeps the masking sum for rows w, w+4, w+8, w+12.
 __global__ __launch_bounds__(FRONT_NT) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
-    __shared__ double2 buf[1024];          // 16 KB: spectrum / masker list / MDCT scratch
+    __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
+    __shared__ double xs[PAC_N];           // 16 KB: sine-windowed block, then per-wave beta rows
     __shared__ int cnt[16];
     __shared__ double red[4];
     const int tid = threadIdx.x;
@@ -94,48 +147,47 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_front(PacSource src, const 
     const int w = tid / WAVE;
     const int64_t g = blockIdx.x;
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
-
-    // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
-    auto dsh = [&](int i) { return __dmul_rn(__dmul_rn(sample(r, i), T->sine[i]), T->hann[i]); };
-    grp_spectrum_mag<FRONT_NT>(dsh, T, buf, tid);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
-    if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
-    double thr[4];
-#pragma unroll 1
-    for (int i = 0; i < 4; ++i) thr[i] = wave_masking_row(buf, nm, T, lane, w + 4 * i);
+    grp_stage_sine<FRONT_NT>(r, T, xs, tid);
     __syncthreads();
 
-    // --- MDCT of the sine-windowed block --------------------------------
+    // --- MDCT of the sine-windowed block, overall scale, band peaks ------
     double* X = reinterpret_cast<double*>(buf + 512);
-    auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
-    grp_mdct<FRONT_NT>(xs, T, buf, X, tid);
+    grp_mdct<FRONT_NT>([&](int i) { return xs[i]; }, T, buf, X, tid);
+    double x[4];
     double mx = 0.0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mx = fmax(mx, fabs(X[j * FRONT_NT + tid]));
+    for (int i = 0; i < 4; ++i) {
+        x[i] = X[(w + 4 * i) * WAVE + lane];
+        mx = fmax(mx, fabs(x[i]));
+    }
     mx = block_max_256(mx, red);
     const int overall = pac_scale_factor(mx, 5);
-    const double gain = (double)(1 << overall);
-
-    // --- SMR (Origin psychoac.py:281-314): SPL(4 (X/2^s)^2) - thr ---------
-    double* d = reinterpret_cast<double*>(buf);     // 1024 doubles (first 8 KB)
+    // band peak |line| of the SCALED lines: max|X| * 2^overall (exact scaling)
+    {
+        double* ax = reinterpret_cast<double*>(buf);
 #pragma unroll
+        for (int i = 0; i < 4; ++i) ax[(w + 4 * i) * WAVE + lane] = fabs(x[i]);
+        __syncthreads();
+        grp_band_max(T, ax, w, lane, W.bandpeak + g, G, (double)(1 << overall), true);
+        __syncthreads();
+    }
+
+    // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
+    grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf, tid);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
+    if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
+    double smr[4];
+#pragma unroll 1
     for (int i = 0; i < 4; ++i) {
-        int l = (w + 4 * i) * WAVE + lane;
-        double x = X[l];                        // unscaled; (x*2^s)/2^s == x exactly
-        d[l] = pac_spl(4.0 * (x * x)) - thr[i];
+        const double thr = wave_masking_row(buf, nm, T, lane, w + 4 * i, xs + w * 512);
+        smr[i] = pac_spl(4.0 * (x[i] * x[i])) - thr;    // Origin psychoac.py:281-314
     }
     __syncthreads();
-    // band peak |line| of the SCALED lines, for the scale factors
-    if (tid < PAC_NB) {
-        int lo = T->lower[tid], n = T->nlines[tid];
-        double sm = -INFINITY, pk = 0.0;
-        for (int l = lo; l < lo + n; ++l) {
-            sm = fmax(sm, d[l]);
-            pk = fmax(pk, fabs(X[l] * gain));
-        }
-        W.smr[tid * G + g] = n ? sm : 0.0;
-        W.bandpeak[tid * G + g] = pk;
-    }
+    double* d = reinterpret_cast<double*>(buf);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[(w + 4 * i) * WAVE + lane] = smr[i];
+    __syncthreads();
+    grp_band_max(T, d, w, lane, W.smr + g, G, 1.0, true);
     if (tid == 0) W.overall[g] = (uint8_t)overall;
 }
 
@@ -324,8 +376,9 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
         bas[tid] = W.ba[tid * G + g];
         sfs[tid] = W.sf[tid * G + g];
     }
-    auto xs = [&](int i) { return __dmul_rn(sample(r, i), T->sine[i]); };
-    grp_mdct<FRONT_NT>(xs, T, buf, X, tid);      // identical to the front kernel's lines
+    const BlockPcm xp(r);
+    grp_mdct<FRONT_NT>([&](int i) { return __dmul_rn(xp(i), T->sine[i]); }, T, buf, X, tid);
+    // (same arithmetic as the front kernel's staged xs: identical lines)
     if (tid == 0) {
         int p = 4;
         for (int b = 0; b < PAC_NB; ++b) { start[b] = p; p += 8 + bas[b] * T->nlines[b]; }
@@ -366,12 +419,13 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
                                                         double* __restrict__ thr_out,
                                                         int32_t* __restrict__ npeaks) {
     __shared__ double2 buf[1024];
+    __shared__ double beta[512];
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
-    wave_spectrum_mag([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, lane);
+    wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, lane);
     int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane);
     double thr[16];
-    wave_masking(buf, nm, T, lane, thr);
+    wave_masking(buf, nm, T, lane, thr, beta);
 #pragma unroll
     for (int q = 0; q < 16; ++q) thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = thr[q];
     if (lane == 0) npeaks[blockIdx.x] = nm;

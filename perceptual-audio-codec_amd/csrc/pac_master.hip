@@ -31,13 +31,13 @@ struct PacMasterWork {
 // LRMS-variant signals: the in-place window chains of EncodeDualChannel and
 // getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
 // M = (a+b)/2, S = (a-b)/2; v2 = M*hann, v3 = S*hann, v4 = (M*hann)*hann, ...
-__device__ __forceinline__ double variant_sample(const BlockRef& rL, const BlockRef& rR,
+__device__ __forceinline__ double variant_sample(const BlockPcm& rL, const BlockPcm& rR,
                                                  const PacTables* __restrict__ T, int v, int i) {
     const double h = T->hann[i];
-    if (v == 1) return __dmul_rn(__dmul_rn(sample(rR, i), T->sine[i]), h);
-    const double a = __dmul_rn(__dmul_rn(sample(rL, i), T->sine[i]), h);
+    if (v == 1) return __dmul_rn(__dmul_rn(rR(i), T->sine[i]), h);
+    const double a = __dmul_rn(__dmul_rn(rL(i), T->sine[i]), h);
     if (v == 0) return a;
-    const double b = __dmul_rn(__dmul_rn(sample(rR, i), T->sine[i]), h);
+    const double b = __dmul_rn(__dmul_rn(rR(i), T->sine[i]), h);
     double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
     ms = __dmul_rn(ms, h);
     if (v >= 4) ms = __dmul_rn(ms, h);
@@ -47,22 +47,23 @@ __device__ __forceinline__ double variant_sample(const BlockRef& rL, const Block
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
                                                          PacMasterWork W, int64_t gb0) {
     __shared__ double2 buf[1024];
+    __shared__ double beta[4 * 512];
     __shared__ int cnt[16];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
     const int64_t j = blockIdx.x / 6;          // block within the chunk
     const int v = blockIdx.x % 6;
-    const BlockRef rL = locate(src, gb0 + j, 0);
-    const BlockRef rR = locate(src, gb0 + j, 1);
+    const BlockPcm rL(locate(src, gb0 + j, 0));
+    const BlockPcm rR(locate(src, gb0 + j, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
-    grp_spectrum_mag<FRONT_NT>(d, T, buf, tid);
+    grp_spectrum_pow<FRONT_NT>(d, T, buf, tid);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, cnt);
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
 #pragma unroll 1
     for (int i = 0; i < 4; ++i) {
         int r = w + 4 * i;
-        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r);
+        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r, beta + w * 512);
     }
 }
 
@@ -139,12 +140,12 @@ __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTab
     __shared__ uint8_t lrms_s[PAC_NB];
     const int lane = threadIdx.x;
     const int64_t j = blockIdx.x;
-    const BlockRef rL = locate(src, gb0 + j, 0);
-    const BlockRef rR = locate(src, gb0 + j, 1);
+    const BlockPcm rL(locate(src, gb0 + j, 0));
+    const BlockPcm rR(locate(src, gb0 + j, 1));
 
     // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:96-102)
-    wave_spectrum_cplx([&](int i) { return sample(rL, i); }, T, bufL, lane);
-    wave_spectrum_cplx([&](int i) { return sample(rR, i); }, T, bufR, lane);
+    wave_spectrum_cplx([&](int i) { return rL(i); }, T, bufL, lane);
+    wave_spectrum_cplx([&](int i) { return rR(i); }, T, bufR, lane);
     if (lane < PAC_NB) {
         const int lo = T->lower[lane], m = T->nlines[lane];
         auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTab
     // --- MDCT L and R, overall scale factors -------------------------------
     double* XL = reinterpret_cast<double*>(bufL + 512);
     double* XR = reinterpret_cast<double*>(bufR + 512);
-    wave_mdct([&](int i) { return __dmul_rn(sample(rL, i), T->sine[i]); }, T, bufL, XL, lane);
-    wave_mdct([&](int i) { return __dmul_rn(sample(rR, i), T->sine[i]); }, T, bufR, XR, lane);
+    wave_mdct([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufL, XL, lane);
+    wave_mdct([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufR, XR, lane);
     double mxL = 0.0, mxR = 0.0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {

@@ -97,10 +97,12 @@ __device__ __forceinline__ void grp_mdct(const XS& xs, const PacTables* __restri
     grp_sync<NT>();
 }
 
-// |FFT(d)[k]|, k < 1024, of a real 2048-sample block d(i) via a 1024-point
-// complex FFT.  buf: 1024 double2 of LDS; on return buf[k].x = |X[k]|.
+// |FFT(d)[k]|^2, k < 1024, of a real 2048-sample block d(i) via a 1024-point
+// complex FFT.  buf: 1024 double2 of LDS; on return buf[k].x = Re^2 + Im^2.
+// (findpeaks compares |X| and the masker SPL sums |X|^2 (psychoac.py:442-449);
+// both only need the square, so no square root is taken.)
 template <int NT, class DS>
-__device__ __forceinline__ void grp_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
+__device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
                                                  double2* buf, int tid) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
@@ -108,28 +110,32 @@ __device__ __forceinline__ void grp_spectrum_mag(const DS& d, const PacTables* _
         buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
     }
     grp_fft<10, NT>(buf, T->fft_tw, tid);
-    // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k])
+    // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k]).
+    // Pair p < 512 owns bins (p, 1024-p); pair 0 owns the self-paired bins 0 and 512.
 #pragma unroll
-    for (int t0 = 0; t0 <= 512; t0 += NT) {
-        int k = t0 + tid;
-        if (k > 512) continue;
-        int k2 = (1024 - k) & 1023;
-        double2 Za = buf[k], Zb = buf[k2];
-        double mags[2];
+    for (int p0 = 0; p0 < 512; p0 += NT) {
+        const int p = p0 + tid;
+        int kk[2];
+        kk[0] = p;
+        kk[1] = p ? 1024 - p : 512;
+        double2 A[2], Bc[2];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            int kk = side ? k2 : k;
-            double2 A = side ? Zb : Za;   // Z[kk]
-            double2 Bc = side ? Za : Zb;  // Z[M-kk]
-            double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
-            double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
-            double2 wo = cmul(T->rfft_tw[kk], o);
+            A[side] = buf[kk[side]];
+            Bc[side] = buf[(1024 - kk[side]) & 1023];
+        }
+        double pw[2];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            double2 e = make_double2(0.5 * (A[side].x + Bc[side].x), 0.5 * (A[side].y - Bc[side].y));
+            double2 o = make_double2(0.5 * (A[side].x - Bc[side].x), 0.5 * (A[side].y + Bc[side].y));
+            double2 wo = cmul(T->rfft_tw[kk[side]], o);
             double xr = e.x + wo.y;
             double xi = e.y - wo.x;
-            mags[side] = hypot(xr, xi);
+            pw[side] = __builtin_fma(xr, xr, xi * xi);
         }
-        buf[k].x = mags[0];
-        if (k2 != k) buf[k2].x = mags[1];
+        buf[kk[0]].x = pw[0];
+        buf[kk[1]].x = pw[1];
     }
     grp_sync<NT>();
 }
@@ -145,9 +151,9 @@ __device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restr
     grp_mdct<WAVE>(xs, T, buf, X, lane);
 }
 template <class DS>
-__device__ __forceinline__ void wave_spectrum_mag(const DS& d, const PacTables* __restrict__ T,
+__device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
                                                   double2* buf, int lane) {
-    grp_spectrum_mag<WAVE>(d, T, buf, lane);
+    grp_spectrum_pow<WAVE>(d, T, buf, lane);
 }
 
 // Masker list in LDS, structure of arrays over the 16 KB scratch (2048 doubles):
@@ -165,7 +171,8 @@ __device__ __forceinline__ double* mk_B(double2* buf) { return reinterpret_cast<
 __device__ __forceinline__ double* mk_ku(double2* buf) { return reinterpret_cast<double*>(buf) + 1024; }
 __device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<double*>(buf) + 1536; }
 
-// findpeaks (psychoac.py:158-191) on |X| held in buf[k].x, masker SPL from the
+// findpeaks (psychoac.py:158-191) on |X|^2 held in buf[k].x (the floor
+// 10 log10|X| > -30 is the equivalent |X|^2 > T->peak_floor2), masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
 // compacted masker list (ascending bin order) written over buf by a group of
 // NT threads.  cnt: LDS scratch of (1024/WAVE) ints.  Returns the masker count.
@@ -185,13 +192,13 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
         S[j] = 0.0;
         if (k >= 1 && k <= 1022) {
             double m = buf[k].x;
-            pk = m > buf[k - 1].x && m > buf[k + 1].x && 10.0 * log10(m) > -30.0;
+            pk = m > buf[k - 1].x && m > buf[k + 1].x && m > T->peak_floor2;
         }
         if (pk) {
             double s = 0.0;
             if (k >= 3) {
                 int hi = k + 3 < 1024 ? k + 3 : 1024;
-                for (int i = k - 3; i < hi; ++i) { double v = buf[i].x; s = __dadd_rn(s, __dmul_rn(v, v)); }
+                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, buf[i].x);   // builtin sum, from 0
             }
             S[j] = pac_spl(csp * s);
         }
@@ -268,7 +275,8 @@ __device__ __forceinline__ int wave_max_i(int v) {
 //   I(l) = sum_m 10^((spl_m(l) - 96)/10) + Intensity(Thresh(f_l)),  thr = SPL(I)
 // with spl_m(l) = SPL_m + spread(dz) - drop, dz = Bark(f_l) - Bark(f_m).
 // The sum splits by dz (the reference's slope selection, psychoac.py:111-116):
-//   dz >  1/2 (masker below the line): 2^(B_m + ku_m (dz - 1/2))   per-pair exp2;
+//   dz >  1/2 (masker below the line): 2^(beta_m + ku_m (z_l - z_r)) per pair,
+//              beta_m = B_m + ku_m ((z_r - z_m) - 1/2) once per (row, masker);
 //              a leading run of maskers whose largest term over the row is
 //              below 2^-64 of a lower bound of every line's total is skipped;
 //   |dz| <= 1/2 (flat):                E_m = 2^B_m                no exp;
@@ -276,14 +284,16 @@ __device__ __forceinline__ int wave_max_i(int v) {
 //              -- the lower slope is the constant -27 dB/Bark, so these terms
 //              factor into per-row suffix sums over maskers (one exp2 per
 //              masker per row instead of per line), exponents in double-double.
-// Values agree with the direct ascending sum to ~1e-15 relative.  Lane owns
-// lines l = 64 r + lane, rows r = 0..15.
-__device__ __forceinline__ double wave_masking_row(double2* buf, int nm, const PacTables* __restrict__ T,
-                                                   int lane, int r) {
-    const double* mz = mk_z(buf);
-    const double* mB = mk_B(buf);
-    const double* mku = mk_ku(buf);
-    const double* mE = mk_E(buf);
+// Every line adds its terms in ascending masker order; the loops are split so
+// that only the ragged ends of each zone need a per-lane test.  Values agree
+// with the direct sum to ~1e-15 relative.  Lane owns line l = 64 r + lane.
+// beta: 512 doubles of LDS private to the calling wave.
+__device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, const PacTables* __restrict__ T,
+                                                   int lane, int r, double* beta) {
+    const double* mz = mk_z(const_cast<double2*>(buf));
+    const double* mB = mk_B(const_cast<double2*>(buf));
+    const double* mku = mk_ku(const_cast<double2*>(buf));
+    const double* mE = mk_E(const_cast<double2*>(buf));
     const int l = r * WAVE + lane;
     const double zl = T->bark_line[l];
     const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
@@ -323,20 +333,27 @@ __device__ __forceinline__ double wave_masking_row(double2* buf, int nm, const P
         dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
         lower = sv * pac_exp2_dd(h, lo2);
     }
-    // --- flat zone, ascending
+    // --- flat zone [U, V), ascending: ragged head, common middle, ragged tail
     double flat = 0.0;
-    const int umin = wave_min_i(U), vmax = wave_max_i(V);
-    for (int m = umin; m < vmax; ++m) {
-        double e = mE[m];
-        if (m >= U && m < V) flat += e;
+    const int umin = wave_min_i(U), umax = wave_max_i(U), vmax = wave_max_i(V);
+    const int fa = umax < vmax ? umax : vmax;
+    const int fb = fa > vmin ? fa : vmin;
+    for (int m = umin; m < fa; ++m) {
+        const double e = mE[m];
+        flat += (m >= U && m < V) ? e : 0.0;
+    }
+    for (int m = fa; m < fb; ++m) flat += mE[m];   // U <= umax <= m < vmin <= V on every lane
+    for (int m = fb; m < vmax; ++m) {
+        const double e = mE[m];
+        flat += (m >= U && m < V) ? e : 0.0;
     }
     // --- upper side, ascending
     const double tiq = T->tiq[l];
     double lb = tiq + flat + lower;                       // I(l) >= lb
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
-    const double l2cut = log2(lb) - 64.0;
-    const int umax = wave_max_i(U);
+    // floor(log2 lb) - 64 from the exponent field: a conservative cut
+    const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
     int m0 = 0;
     for (; m0 < umax; ++m0) {         // leading negligible maskers (wave-uniform test)
         const double ku = mku[m0];
@@ -344,19 +361,26 @@ __device__ __forceinline__ double wave_masking_row(double2* buf, int nm, const P
         const int keep = !(ku < 0.0 && t < l2cut);
         if (__builtin_amdgcn_readfirstlane(keep)) break;
     }
+    for (int m = m0 + lane; m < umax; m += WAVE)
+        beta[m] = __builtin_fma((zr - mz[m]) - 0.5, mku[m], mB[m]);
+    wave_sync();
+    const double dl = zl - zr;
     double up = 0.0;
+    const int ua = umin > m0 ? (umin < umax ? umin : umax) : m0;
 #pragma unroll 4
-    for (int m = m0; m < umax; ++m) {
-        const double a = (zl - mz[m]) - 0.5;
-        const double t = pac_exp2(__builtin_fma(a, mku[m], mB[m]));
+    for (int m = m0; m < ua; ++m)                   // m < umin <= U on every lane
+        up += pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
+    for (int m = ua; m < umax; ++m) {
+        const double t = pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
         up += (m < U) ? t : 0.0;
     }
+    wave_sync();                                    // beta is rewritten by the next row
     return pac_spl(((up + flat) + lower) + tiq);
 }
 
 // all 16 rows by one wave
-__device__ __forceinline__ void wave_masking(double2* buf, int nm, const PacTables* __restrict__ T,
-                                             int lane, double thr[16]) {
+__device__ __forceinline__ void wave_masking(const double2* buf, int nm, const PacTables* __restrict__ T,
+                                             int lane, double thr[16], double* beta) {
 #pragma unroll 1
-    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r);
+    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r, beta);
 }

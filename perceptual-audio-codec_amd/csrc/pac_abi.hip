@@ -128,6 +128,7 @@ static void build_tables(int fs, PacTables* t) {
         while (10.0 * log10(nextafter(m, 1.0)) <= -30.0) m = nextafter(m, 1.0);
         t->peak_floor2 = m * m;
     }
+    for (int i = 1; i < 32; i++) t->inv_int[i] = 1.0 / (double)i;
     const int step = fs / PAC_N;  // Py2 integer division, psychoac.py:188
     double mx = -1.0;
     for (int k = 0; k < PAC_HALFN; k++) {

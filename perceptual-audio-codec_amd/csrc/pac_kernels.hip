@@ -136,12 +136,14 @@ __device__ __forceinline__ void grp_band_max(const PacTables* __restrict__ T, co
 // into LDS; the MDCT runs first (lines kept in registers, band peaks taken),
 // then the Hann spectrum whose masker list the four waves share; each wave
 // sweeps the masking sum for rows w, w+4, w+8, w+12.
-__global__ __launch_bounds__(FRONT_NT) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
+__global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
     __shared__ double xs[PAC_N];           // 16 KB: sine-windowed block, then per-wave beta rows
-    __shared__ int cnt[16];
-    __shared__ double red[4];
+    // exactly 32 KB of LDS (5 workgroups per CU): the small reduction scratch
+    // lives in whichever region is idle at that point
+    double* red = reinterpret_cast<double*>(buf);  // MDCT scratch, free once the lines are out
+    int* cnt = reinterpret_cast<int*>(xs);         // free once the spectrum input is staged
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;

@@ -165,6 +165,8 @@ __device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* 
 #define PAC_LOG2_10_OVER_10 0.33219280948873624   // log2(10)/10
 #define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
 #define PAC_LN2 0.6931471805599453
+#define PAC_MOM_MIN 24      // fewest common upper maskers for the moment form
+#define PAC_MOM_DMAX 24     // highest Taylor degree of the moment form
 
 __device__ __forceinline__ double* mk_z(double2* buf) { return reinterpret_cast<double*>(buf); }
 __device__ __forceinline__ double* mk_B(double2* buf) { return reinterpret_cast<double*>(buf) + 512; }
@@ -232,7 +234,7 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
         }
     }
     grp_sync<NT>();
-    return tot;
+    return __builtin_amdgcn_readfirstlane(tot);
 }
 
 __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
@@ -260,15 +262,16 @@ __device__ __forceinline__ void dd_affine(double c, double k, double a, double b
     lo = e2 + pl;
 }
 
+// wave-uniform results, returned in scalar registers (uniform loop bounds)
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w < v ? w : v; }
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w > v ? w : v; }
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 // Masking threshold (psychoac.py:447-456): for each MDCT line
@@ -354,22 +357,79 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
     for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
     // floor(log2 lb) - 64 from the exponent field: a conservative cut
     const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
-    int m0 = 0;
-    for (; m0 < umax; ++m0) {         // leading negligible maskers (wave-uniform test)
-        const double ku = mku[m0];
-        const double t = __builtin_fma(fmax((zr - mz[m0]) - 0.5, 0.0), ku, mB[m0]);
-        const int keep = !(ku < 0.0 && t < l2cut);
-        if (__builtin_amdgcn_readfirstlane(keep)) break;
+    int m0 = umax;                    // first masker that is not negligible (64 tested at once)
+    for (int base = 0; base < umax; base += WAVE) {
+        const int m = base + lane;
+        int keep = 1;
+        if (m < umax) {
+            const double ku = mku[m];
+            const double t = __builtin_fma(fmax((zr - mz[m]) - 0.5, 0.0), ku, mB[m]);
+            keep = !(ku < 0.0 && t < l2cut);
+        }
+        const unsigned long long kb = __ballot(keep);
+        if (kb) { m0 = base + __builtin_ctzll(kb); break; }
     }
+    m0 = __builtin_amdgcn_readfirstlane(m0 < umax ? m0 : umax);
+    // exponents relative to the row middle: 2^(beta_m + ku_m (z_l - z_mid))
+    const double zm = 0.5 * (zr + T->bark_line[r * WAVE + WAVE - 1]);
     for (int m = m0 + lane; m < umax; m += WAVE)
-        beta[m] = __builtin_fma((zr - mz[m]) - 0.5, mku[m], mB[m]);
+        beta[m] = __builtin_fma((zm - mz[m]) - 0.5, mku[m], mB[m]);
     wave_sync();
-    const double dl = zl - zr;
+    const double dl = zl - zm;
     double up = 0.0;
     const int ua = umin > m0 ? (umin < umax ? umin : umax) : m0;
+    // Maskers [m0, ua) lie below every line of the row.  Their sum factors as
+    //   2^(kc dl) * sum_d (dl ln2)^d / d! * S_d,   S_d = sum_m 2^beta_m (ku_m - kc)^d,
+    // kc the middle of their slopes: the Taylor series of 2^((ku_m - kc) dl),
+    // truncated where its remainder is below 2^-57 of every term.
+    bool direct = true;
+    if (ua - m0 >= PAC_MOM_MIN) {
+        double kmn = INFINITY, kmx = -INFINITY;
+        for (int m = m0 + lane; m < ua; m += WAVE) {
+            const double k = mku[m];
+            kmn = fmin(kmn, k);
+            kmx = fmax(kmx, k);
+        }
+        double adl = fabs(dl);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            kmn = fmin(kmn, __shfl_xor(kmn, o, WAVE));
+            kmx = fmax(kmx, __shfl_xor(kmx, o, WAVE));
+            adl = fmax(adl, __shfl_xor(adl, o, WAVE));
+        }
+        const double kc = 0.5 * (kmn + kmx);
+        const double eps = (0.5 * (kmx - kmn) * adl) * PAC_LN2 * 1.0000001;
+        // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57
+        int D = 0;
+        double rem = pac_exp2(eps * 1.4426950408889634) * eps;  // e^eps eps^1/1!
+        while (rem > 0x1p-57 && D < PAC_MOM_DMAX + 1) { ++D; rem *= eps / (double)(D + 1); }
+        D = __builtin_amdgcn_readfirstlane(D);
+        if (D <= PAC_MOM_DMAX) {
+            direct = false;
+            for (int m = m0 + lane; m < ua; m += WAVE) beta[m] = pac_exp2(beta[m]);   // own slots
+            const double x = dl * PAC_LN2;
+            double acc = 0.0, q = 1.0;
+            for (int d = 0; d <= D; ++d) {
+                double part = 0.0;
+                for (int m = m0 + lane; m < ua; m += WAVE) {
+                    const double p = beta[m];
+                    part += p;
+                    beta[m] = p * (mku[m] - kc);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, WAVE);
+                acc = __builtin_fma(part, q, acc);
+                q = (q * x) * T->inv_int[d + 1];
+            }
+            up = acc * pac_exp2(kc * dl);
+        }
+    }
+    if (direct) {
 #pragma unroll 4
-    for (int m = m0; m < ua; ++m)                   // m < umin <= U on every lane
-        up += pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
+        for (int m = m0; m < ua; ++m)               // m < umin <= U on every lane
+            up += pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
+    }
+#pragma unroll 2
     for (int m = ua; m < umax; ++m) {
         const double t = pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
         up += (m < U) ? t : 0.0;

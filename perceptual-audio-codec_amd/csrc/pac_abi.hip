@@ -107,8 +107,10 @@ static void build_tables(int fs, PacTables* t) {
         t->mdct_pre[q] = make_double2(cos(a), sin(a));
         double b = -M_PI * q / M;
         t->mdct_post[q] = make_double2(cos(b), sin(b));
-        double c = -2.0 * M_PI * q / 1024.0;
-        t->fft_tw[q] = make_double2(cos(c), sin(c));
+    }
+    for (int k = 0; k < PAC_HALFN; k++) {
+        double c = -2.0 * M_PI * k / 1024.0;
+        t->fft_tw[k] = make_double2(cos(c), sin(c));
     }
     for (int k = 0; k < PAC_HALFN; k++) {
         double a = -2.0 * M_PI * k / 2048.0;

@@ -19,7 +19,7 @@ struct PacTables {
     double hann[PAC_N];           // window.py:41-53
     double2 mdct_pre[PAC_HALFN / 2];   // exp(-i pi (q+1/4)/M)   (DCT-IV fold, M=1024)
     double2 mdct_post[PAC_HALFN / 2];  // exp(-i pi q / M)
-    double2 fft_tw[PAC_HALFN / 2];     // exp(-2 pi i k / 1024), k < 512
+    double2 fft_tw[PAC_HALFN];         // exp(-2 pi i k / 1024), k < 1024
     double2 rfft_tw[PAC_HALFN];        // exp(-2 pi i k / 2048), k < 1024
     double bark_line[PAC_HALFN];  // Bark(MDCTFreqs)                psychoac.py:434,95
     double tiq[PAC_HALFN];        // Intensity(Thresh(MDCTFreqs))   psychoac.py:437

@@ -139,10 +139,10 @@ __device__ __forceinline__ void grp_band_max(const PacTables* __restrict__ T, co
 __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
-    __shared__ double xs[PAC_N];           // 16 KB: sine-windowed block, then per-wave beta rows
+    __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then per-wave beta rows
     // exactly 32 KB of LDS (5 workgroups per CU): the small reduction scratch
     // lives in whichever region is idle at that point
-    double* red = reinterpret_cast<double*>(buf);  // MDCT scratch, free once the lines are out
+    double* red = reinterpret_cast<double*>(buf + 512);  // MDCT scratch, free once the lines are out
     int* cnt = reinterpret_cast<int*>(xs);         // free once the spectrum input is staged
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -153,8 +153,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     __syncthreads();
 
     // --- MDCT of the sine-windowed block, overall scale, band peaks ------
-    double* X = reinterpret_cast<double*>(buf + 512);
-    grp_mdct<FRONT_NT>([&](int i) { return xs[i]; }, T, buf, X, tid);
+    const double* X = grp_mdct<FRONT_NT>([&](int i) { return xs[i]; }, T, buf, tid);
     double x[4];
     double mx = 0.0;
 #pragma unroll
@@ -166,7 +165,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     const int overall = pac_scale_factor(mx, 5);
     // band peak |line| of the SCALED lines: max|X| * 2^overall (exact scaling)
     {
-        double* ax = reinterpret_cast<double*>(buf);
+        double* ax = reinterpret_cast<double*>(buf + 512);
 #pragma unroll
         for (int i = 0; i < 4; ++i) ax[(w + 4 * i) * WAVE + lane] = fabs(x[i]);
         __syncthreads();
@@ -175,7 +174,8 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     }
 
     // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
-    grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf, tid);
+    grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf,
+                               reinterpret_cast<double2*>(xs), tid);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     double smr[4];
@@ -365,8 +365,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
                                                           PacOriginWork W, int64_t G,
                                                           const int64_t* __restrict__ off,
                                                           uint8_t* __restrict__ out) {
-    __shared__ double2 buf[512];
-    __shared__ double X[1024];
+    __shared__ double2 buf[1024];        // MDCT: lines in the first 8 KB
     __shared__ uint32_t words[PACK_WORDS];
     __shared__ int start[PAC_NB];
     __shared__ int bas[PAC_NB], sfs[PAC_NB];
@@ -379,7 +378,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
         sfs[tid] = W.sf[tid * G + g];
     }
     const BlockPcm xp(r);
-    grp_mdct<FRONT_NT>([&](int i) { return __dmul_rn(xp(i), T->sine[i]); }, T, buf, X, tid);
+    const double* X = grp_mdct<FRONT_NT>([&](int i) { return __dmul_rn(xp(i), T->sine[i]); }, T, buf, tid);
     // (same arithmetic as the front kernel's staged xs: identical lines)
     if (tid == 0) {
         int p = 4;
@@ -421,10 +420,11 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
                                                         double* __restrict__ thr_out,
                                                         int32_t* __restrict__ npeaks) {
     __shared__ double2 buf[1024];
+    __shared__ double2 tmp[1024];
     __shared__ double beta[512];
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
-    wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, lane);
+    wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
     int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane);
     double thr[16];
     wave_masking(buf, nm, T, lane, thr, beta);
@@ -436,11 +436,10 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
 // MDCT probe: mdct.py:49-82 of n raw (unwindowed) blocks, sine window applied
 __global__ __launch_bounds__(64) void k_debug_mdct(const PacTables* __restrict__ T,
                                                    const double* __restrict__ data, double* __restrict__ X) {
-    __shared__ double2 buf[512];
-    __shared__ double Xs[1024];
+    __shared__ double2 buf[1024];
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
-    wave_mdct([&](int i) { return __dmul_rn(d[i], T->sine[i]); }, T, buf, Xs, lane);
+    const double* Xs = wave_mdct([&](int i) { return __dmul_rn(d[i], T->sine[i]); }, T, buf, lane);
     for (int k = lane; k < PAC_HALFN; k += WAVE) X[(int64_t)blockIdx.x * PAC_HALFN + k] = Xs[k];
 }
 

@@ -47,7 +47,7 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
                                                          PacMasterWork W, int64_t gb0) {
     __shared__ double2 buf[1024];
-    __shared__ double beta[4 * 512];
+    __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // spectrum FFT scratch, then beta rows
     __shared__ int cnt[16];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const BlockPcm rL(locate(src, gb0 + j, 0));
     const BlockPcm rR(locate(src, gb0 + j, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
-    grp_spectrum_pow<FRONT_NT>(d, T, buf, tid);
+    grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, cnt);
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
 #pragma unroll 1
@@ -169,10 +169,8 @@ __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTab
     wave_sync();
 
     // --- MDCT L and R, overall scale factors -------------------------------
-    double* XL = reinterpret_cast<double*>(bufL + 512);
-    double* XR = reinterpret_cast<double*>(bufR + 512);
-    wave_mdct([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufL, XL, lane);
-    wave_mdct([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufR, XR, lane);
+    double* XL = wave_mdct([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufL, lane);
+    double* XR = wave_mdct([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufR, lane);
     double mxL = 0.0, mxR = 0.0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -186,8 +184,8 @@ __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTab
     if (lane == 0) { W.overall[j * 2] = (uint8_t)oL; W.overall[j * 2 + 1] = (uint8_t)oR; }
 
     // --- per-line SMR terms (psychoac.py:533-597) ---------------------------
-    double* dLR0 = reinterpret_cast<double*>(bufL);     // first 8 KB of each buffer
-    double* dLR1 = reinterpret_cast<double*>(bufR);
+    double* dLR0 = reinterpret_cast<double*>(bufL + 512);   // second 8 KB of each buffer
+    double* dLR1 = reinterpret_cast<double*>(bufR + 512);
     const double* thr = W.thr + j * 6 * PAC_HALFN;
     double* lines = W.lines + j * 2 * PAC_HALFN;
     double dM[16], dS[16];

@@ -64,14 +64,71 @@ __device__ __forceinline__ void grp_fft(double2* buf, const double2* __restrict_
     grp_sync<NT>();
 }
 
+// Self-sorting (Stockham) FFT of n = 2^LOG complex values in natural order,
+// radix-4 stages (+ one radix-2 stage for odd LOG), ping-ponging between src
+// and dst; every read is unit-stride across lanes and no bit-reversal
+// permutation is needed.  Returns the buffer holding the result (always dst:
+// LOG = 10 has 5 stages, LOG = 9 has 4 + 1).  tw[k] = exp(-2 pi i k / 1024).
+template <int LOG, int NT>
+__device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
+                                                     const double2* __restrict__ tw, int tid) {
+    constexpr int N = 1 << LOG;
+    constexpr int N4 = N / 4;
+#pragma unroll
+    for (int st = 0; st < LOG / 2; ++st) {
+        const int Ns = 1 << (2 * st);
+        grp_sync<NT>();
+#pragma unroll
+        for (int j0 = 0; j0 < N4; j0 += NT) {
+            const int j = j0 + tid;
+            if (N4 % NT != 0 && j >= N4) break;
+            const int k = j & (Ns - 1);
+            double2 v0 = src[j], v1 = src[j + N4], v2 = src[j + 2 * N4], v3 = src[j + 3 * N4];
+            if (Ns > 1) {
+                const int e = k * (256 / Ns);           // angle -2 pi k r / (4 Ns)
+                v1 = cmul(v1, tw[e]);
+                v2 = cmul(v2, tw[2 * e]);
+                v3 = cmul(v3, tw[3 * e]);
+            }
+            const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
+            const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
+            const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
+            const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);   // -i (v1 - v3)
+            const int o = ((j - k) << 2) + k;
+            dst[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
+            dst[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
+            dst[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
+            dst[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+        }
+        double2* t = src; src = dst; dst = t;
+    }
+    if (LOG & 1) {                                     // last stage, radix 2, Ns = N/2
+        grp_sync<NT>();
+#pragma unroll
+        for (int j0 = 0; j0 < N / 2; j0 += NT) {
+            const int j = j0 + tid;
+            if ((N / 2) % NT != 0 && j >= N / 2) break;
+            const double2 v0 = src[j];
+            const double2 v1 = cmul(src[j + N / 2], tw[j * (1024 / N)]);
+            dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
+            dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
+        }
+        double2* t = src; src = dst; dst = t;
+    }
+    grp_sync<NT>();
+    return src;
+}
+
 // MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
 // sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
 // place in codec.py:240).  Evaluated as DCT-IV of the folded block with a
-// 512-point complex FFT.  buf: 512 double2 of LDS scratch.  Output: X[1024]
-// in LDS.  An exactly-zero line keeps the reference's sign (mdct_zero_neg).
+// 512-point complex Stockham FFT.  buf: 1024 double2 of LDS.  Output: the
+// 1024 lines as doubles in the first 8 KB of buf (X = (double*)buf); the
+// second 8 KB is free scratch on return.  An exactly-zero line keeps the
+// reference's sign (mdct_zero_neg).
 template <int NT, class XS>
-__device__ __forceinline__ void grp_mdct(const XS& xs, const PacTables* __restrict__ T,
-                                         double2* buf, double* X, int tid) {
+__device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                            double2* buf, int tid) {
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
         int q = q0 + tid;
@@ -81,13 +138,14 @@ __device__ __forceinline__ void grp_mdct(const XS& xs, const PacTables* __restri
                              : __dsub_rn(xs(n0 - 512), xs(1535 - n0));
         double u1 = n1 < 512 ? __dsub_rn(-xs(1535 - n1), xs(1536 + n1))
                              : __dsub_rn(xs(n1 - 512), xs(1535 - n1));
-        buf[brev(q, 9)] = cmul(make_double2(u0, u1), T->mdct_pre[q]);
+        buf[q] = cmul(make_double2(u0, u1), T->mdct_pre[q]);
     }
-    grp_fft<9, NT>(buf, T->fft_tw, tid);
+    const double2* Y = grp_fft_stockham<9, NT>(buf, buf + 512, T->fft_tw, tid);   // = buf + 512
+    double* X = reinterpret_cast<double*>(buf);
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
         int q = q0 + tid;
-        double2 y = cmul(buf[q], T->mdct_post[q]);
+        double2 y = cmul(Y[q], T->mdct_post[q]);
         double x0 = y.x * (1.0 / 1024.0), x1 = -y.y * (1.0 / 1024.0);
         if (x0 == 0.0) x0 = T->mdct_zero_neg[2 * q] ? -0.0 : 0.0;
         if (x1 == 0.0) x1 = T->mdct_zero_neg[1023 - 2 * q] ? -0.0 : 0.0;
@@ -95,21 +153,23 @@ __device__ __forceinline__ void grp_mdct(const XS& xs, const PacTables* __restri
         X[1023 - 2 * q] = x1;
     }
     grp_sync<NT>();
+    return X;
 }
 
 // |FFT(d)[k]|^2, k < 1024, of a real 2048-sample block d(i) via a 1024-point
-// complex FFT.  buf: 1024 double2 of LDS; on return buf[k].x = Re^2 + Im^2.
-// (findpeaks compares |X| and the masker SPL sums |X|^2 (psychoac.py:442-449);
-// both only need the square, so no square root is taken.)
+// complex Stockham FFT.  buf and tmp: 1024 double2 of LDS each; the input
+// pairs are staged in buf, the FFT ends in tmp, and on return
+// buf[k].x = Re^2 + Im^2 (tmp is free again).  (findpeaks compares |X| and
+// the masker SPL sums |X|^2 (psychoac.py:442-449); both only need the square.)
 template <int NT, class DS>
 __device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
-                                                 double2* buf, int tid) {
+                                                 double2* buf, double2* tmp, int tid) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
         int n = n0 + tid;
-        buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
+        buf[n] = make_double2(d(2 * n), d(2 * n + 1));
     }
-    grp_fft<10, NT>(buf, T->fft_tw, tid);
+    const double2* Z = grp_fft_stockham<10, NT>(buf, tmp, T->fft_tw, tid);   // = tmp
     // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k]).
     // Pair p < 512 owns bins (p, 1024-p); pair 0 owns the self-paired bins 0 and 512.
 #pragma unroll
@@ -118,24 +178,17 @@ __device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* _
         int kk[2];
         kk[0] = p;
         kk[1] = p ? 1024 - p : 512;
-        double2 A[2], Bc[2];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            A[side] = buf[kk[side]];
-            Bc[side] = buf[(1024 - kk[side]) & 1023];
-        }
-        double pw[2];
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            double2 e = make_double2(0.5 * (A[side].x + Bc[side].x), 0.5 * (A[side].y - Bc[side].y));
-            double2 o = make_double2(0.5 * (A[side].x - Bc[side].x), 0.5 * (A[side].y + Bc[side].y));
+            const double2 A = Z[kk[side]];
+            const double2 Bc = Z[(1024 - kk[side]) & 1023];
+            double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
+            double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
             double2 wo = cmul(T->rfft_tw[kk[side]], o);
             double xr = e.x + wo.y;
             double xi = e.y - wo.x;
-            pw[side] = __builtin_fma(xr, xr, xi * xi);
+            buf[kk[side]].x = __builtin_fma(xr, xr, xi * xi);
         }
-        buf[kk[0]].x = pw[0];
-        buf[kk[1]].x = pw[1];
     }
     grp_sync<NT>();
 }
@@ -146,14 +199,14 @@ __device__ __forceinline__ void wave_fft(double2* buf, const double2* __restrict
     grp_fft<LOG, WAVE>(buf, tw, lane);
 }
 template <class XS>
-__device__ __forceinline__ void wave_mdct(const XS& xs, const PacTables* __restrict__ T,
-                                          double2* buf, double* X, int lane) {
-    grp_mdct<WAVE>(xs, T, buf, X, lane);
+__device__ __forceinline__ double* wave_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                             double2* buf, int lane) {
+    return grp_mdct<WAVE>(xs, T, buf, lane);
 }
 template <class DS>
 __device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
-                                                  double2* buf, int lane) {
-    grp_spectrum_pow<WAVE>(d, T, buf, lane);
+                                                  double2* buf, double2* tmp, int lane) {
+    grp_spectrum_pow<WAVE>(d, T, buf, tmp, lane);
 }
 
 // Masker list in LDS, structure of arrays over the 16 KB scratch (2048 doubles):

@@ -685,7 +685,7 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
                 if (ba) ba++;
                 fields->ba[ch][b] = ba;
                 fields->sf[ch][b] = (int32_t)br.get(4);
-                fields->smr[ch][b] = master ? smr[ch * PAC_NB + b] : smr[b * G + ch];
+                fields->smr[ch][b] = smr[ch * PAC_NB + b];
                 if (!master) {
                     for (int l = 0; l < nl[b]; l++) fields->mant[ch][line + l] = ba ? (int32_t)br.get(ba) : 0;
                 } else if (ba) {

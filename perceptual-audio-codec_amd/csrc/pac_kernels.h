@@ -13,13 +13,14 @@ struct PacSource {
     int dbg;                   // diagnostic phase switches (PAC_DEBUG_FLAGS), 0 in production
 };
 
-// Per-channel-block work arrays (structure of arrays: index [band * G + g]).
+// Per-channel-block work arrays, index [g * 25 + band]: a workgroup writes
+// its channel-block's bands as one contiguous run.
 struct PacOriginWork {
-    double* smr;        // [25][G]
-    double* bandpeak;   // [25][G] max |scaled line| per band
+    double* smr;        // [G][25]
+    double* bandpeak;   // [G][25] max |scaled line| per band
     uint8_t* overall;   // [G]
-    uint8_t* ba;        // [25][G]
-    uint8_t* sf;        // [25][G]
+    uint8_t* ba;        // [G][25]
+    uint8_t* sf;        // [G][25]
     int32_t* nbytes;    // [G] 4 + payload bytes
 };
 

@@ -109,6 +109,16 @@ __device__ __forceinline__ void grp_stage_sine(const BlockRef& r, const PacTable
 
 #define FRONT_NT 256
 
+// Work item of workgroup `bid` out of n such that each of the 8 XCDs (the
+// dispatcher deals workgroups round-robin, bid % 8) sweeps one contiguous
+// range of items: neighbouring channel-blocks -- the two channels of a block
+// and the next block, which re-reads this block's second hop -- then share
+// that XCD's L2 instead of fetching the same PCM lines into several.
+__device__ __forceinline__ int64_t xcd_item(int64_t bid, int64_t n) {
+    const int64_t x = bid & 7, i = bid >> 3, q = n >> 3, r = n & 7;
+    return x * q + (x < r ? x : r) + i;
+}
+
 __device__ __forceinline__ double block_max_256(double v, double* red) {
     v = wave_max(v);
     if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = v;
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
-    const int64_t g = blockIdx.x;
+    const int64_t g = xcd_item(blockIdx.x, G);
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
     grp_stage_sine<FRONT_NT>(r, T, xs, tid);
     __syncthreads();
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
 #pragma unroll
         for (int i = 0; i < 4; ++i) ax[(w + 4 * i) * WAVE + lane] = fabs(x[i]);
         __syncthreads();
-        grp_band_max(T, ax, w, lane, W.bandpeak + g, G, (double)(1 << overall), true);
+        grp_band_max(T, ax, w, lane, W.bandpeak + g * PAC_NB, 1, (double)(1 << overall), true);
         __syncthreads();
     }
 
@@ -189,7 +199,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
 #pragma unroll
     for (int i = 0; i < 4; ++i) d[(w + 4 * i) * WAVE + lane] = smr[i];
     __syncthreads();
-    grp_band_max(T, d, w, lane, W.smr + g, G, 1.0, true);
+    grp_band_max(T, d, w, lane, W.smr + g * PAC_NB, 1, 1.0, true);
     if (tid == 0) W.overall[g] = (uint8_t)overall;
 }
 
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(256) void k_origin_alloc(const PacTables* __restric
     int nl[PAC_NB];
 #pragma unroll
     for (int b = 0; b < PAC_NB; ++b) {
-        nf[b] = W.smr[b * G + g];
+        nf[b] = W.smr[g * PAC_NB + b];
         alloc[b] = 0;
         nl[b] = T->nlines[b];
     }
@@ -253,8 +263,8 @@ __global__ __launch_bounds__(256) void k_origin_alloc(const PacTables* __restric
         int a = alloc[b];
         if (a < 2) a = 0;
         if (a > maxMantBits) a = maxMantBits;
-        W.ba[b * G + g] = (uint8_t)a;
-        W.sf[b * G + g] = (uint8_t)pac_scale_factor(W.bandpeak[b * G + g], a);
+        W.ba[g * PAC_NB + b] = (uint8_t)a;
+        W.sf[g * PAC_NB + b] = (uint8_t)pac_scale_factor(W.bandpeak[g * PAC_NB + b], a);
         bits += 8 + a * nl[b];
     }
     W.nbytes[g] = 4 + (bits + 7) / 8;
@@ -370,12 +380,12 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
     __shared__ int start[PAC_NB];
     __shared__ int bas[PAC_NB], sfs[PAC_NB];
     const int tid = threadIdx.x;
-    const int64_t g = blockIdx.x;
+    const int64_t g = xcd_item(blockIdx.x, G);
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
     for (int i = tid; i < PACK_WORDS; i += FRONT_NT) words[i] = 0;
     if (tid < PAC_NB) {
-        bas[tid] = W.ba[tid * G + g];
-        sfs[tid] = W.sf[tid * G + g];
+        bas[tid] = W.ba[g * PAC_NB + tid];
+        sfs[tid] = W.sf[g * PAC_NB + tid];
     }
     const BlockPcm xp(r);
     const double* X = grp_mdct<FRONT_NT>([&](int i) { return __dmul_rn(xp(i), T->sine[i]); }, T, buf, tid);

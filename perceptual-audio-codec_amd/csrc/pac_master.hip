@@ -52,8 +52,9 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
-    const int64_t j = blockIdx.x / 6;          // block within the chunk
-    const int v = blockIdx.x % 6;
+    const int64_t item = xcd_item(blockIdx.x, gridDim.x);
+    const int64_t j = item / 6;                // block within the chunk
+    const int v = (int)(item % 6);
     const BlockPcm rL(locate(src, gb0 + j, 0));
     const BlockPcm rR(locate(src, gb0 + j, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };

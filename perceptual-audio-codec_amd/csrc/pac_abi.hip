@@ -187,6 +187,7 @@ struct pac_ctx {
     bool have_huff = false;
     // work
     DevBuf<double> smr, bandpeak;
+    DevBuf<long long> prof;                // PAC_DEBUG_FLAGS & 16: phase clocks
     DevBuf<uint8_t> overall, ba, sf;
     DevBuf<int32_t> nbytes;
     DevBuf<int64_t> off, tile_sums, grand_total, frame_off, blk_off, stream_off;
@@ -235,7 +236,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->base.release();
-    c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release();
+    c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release(); c->prof.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
     c->stream_off.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
@@ -368,6 +369,37 @@ __global__ void k_stream_offsets(const int64_t* __restrict__ off, const int64_t*
     if (s == n_streams) so[s] = *total;
 }
 
+// diagnostic: mean shader-clock cycles per phase of k_origin_front over the
+// sampled workgroups (per wave, and the spread between a workgroup's waves)
+static int report_phase_clocks(pac_ctx* c, hipStream_t s, int64_t n) {
+    std::vector<long long> h(n);
+    HIPCHK(hipMemcpyAsync(h.data(), c->prof.p, n * sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    double mean[PAC_PROF_MARKS] = {0}, spread[PAC_PROF_MARKS] = {0};
+    int64_t cnt = 0;
+    for (int64_t g = 0; g < PAC_PROF_WG; g++) {
+        const long long* t = &h[g * 4 * PAC_PROF_MARKS];
+        if (!t[0]) continue;
+        cnt++;
+        for (int k = 1; k < PAC_PROF_MARKS; k++) {
+            long long mx = 0, mn = 0;
+            for (int w = 0; w < 4; w++) {
+                long long d = t[w * PAC_PROF_MARKS + k] - t[w * PAC_PROF_MARKS + k - 1];
+                mean[k] += d / 4.0;
+                if (w == 0 || d > mx) mx = d;
+                if (w == 0 || d < mn) mn = d;
+            }
+            spread[k] += (double)(mx - mn);
+        }
+    }
+    if (!cnt) return PAC_OK;
+    fprintf(stderr, "PAC_PROF %lld workgroups, mean cycles per phase (wave mean / max-min spread):\n",
+            (long long)cnt);
+    for (int k = 1; k < PAC_PROF_MARKS; k++)
+        fprintf(stderr, "  phase %d: %10.0f  %10.0f\n", k, mean[k] / cnt, spread[k] / cnt);
+    return PAC_OK;
+}
+
 static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src, int64_t G,
                       uint8_t* out_dev, int64_t out_cap, int64_t* out_total, int64_t** off_dev) {
     int rc;
@@ -379,8 +411,15 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     PacOriginWork W{c->smr.p, c->bandpeak.p, c->overall.p, c->ba.p, c->sf.p, c->nbytes.p};
     hipStream_t s = c->stream;
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
+    const int64_t nprof = (int64_t)PAC_PROF_WG * 4 * PAC_PROF_MARKS;
+    if (c->dbg & 16) {
+        if ((rc = c->prof.ensure(nprof))) return rc;
+        HIPCHK(hipMemsetAsync(c->prof.p, 0, nprof * sizeof(long long), s));
+        src.prof = c->prof.p;
+    }
     hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G);
     HIPCHK(hipGetLastError());
+    if (c->dbg & 16) report_phase_clocks(c, s, nprof);
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_origin_alloc, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, T, W, G,
                        bit_budget(p), 16);

@@ -11,7 +11,11 @@ struct PacSource {
     int n_streams;
     int n_ch;
     int dbg;                   // diagnostic phase switches (PAC_DEBUG_FLAGS), 0 in production
+    long long* prof;           // diagnostic per-wave phase clocks (PAC_DEBUG_FLAGS & 16), else null
 };
+
+#define PAC_PROF_WG 4096       // workgroups sampled by the phase clocks
+#define PAC_PROF_MARKS 10
 
 // Per-channel-block work arrays, index [g * 25 + band]: a workgroup writes
 // its channel-block's bands as one contiguous run.

@@ -142,6 +142,22 @@ __device__ __forceinline__ void grp_band_max(const PacTables* __restrict__ T, co
     }
 }
 
+// unsigned keys that order like the doubles (for LDS atomic max)
+__device__ __forceinline__ unsigned long long pac_order_key(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double pac_order_unkey(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// diagnostic: shader clock of wave w at mark k (first PAC_PROF_WG items only)
+#define PROF_MARK(k)                                                                      \
+    do {                                                                                  \
+        if (src.prof && g < PAC_PROF_WG && lane == 0)                                     \
+            src.prof[(g * 4 + w) * PAC_PROF_MARKS + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+
 // One 256-thread workgroup per channel-block.  The block is windowed once
 // into LDS; the MDCT runs first (lines kept in registers, band peaks taken),
 // then the Hann spectrum whose masker list the four waves share; each wave
@@ -152,41 +168,52 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then per-wave beta rows
     // exactly 32 KB of LDS (5 workgroups per CU): the small reduction scratch
     // lives in whichever region is idle at that point
-    double* red = reinterpret_cast<double*>(buf + 512);  // MDCT scratch, free once the lines are out
     int* cnt = reinterpret_cast<int*>(xs);         // free once the spectrum input is staged
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
     const int64_t g = xcd_item(blockIdx.x, G);
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
+    PROF_MARK(0);
     grp_stage_sine<FRONT_NT>(r, T, xs, tid);
     __syncthreads();
+    PROF_MARK(1);
 
     // --- MDCT of the sine-windowed block, overall scale, band peaks ------
     const double* X = grp_mdct<FRONT_NT>([&](int i) { return xs[i]; }, T, buf, tid);
+    PROF_MARK(2);
+    // band peaks (and the block maximum, slot 25) by LDS atomic max on the
+    // bit patterns of |X|, which order like the values
     double x[4];
-    double mx = 0.0;
+    unsigned long long* bk = reinterpret_cast<unsigned long long*>(buf + 512);   // free MDCT half
+    if (tid < PAC_NB + 1) bk[tid] = 0ull;
+    __syncthreads();
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        x[i] = X[(w + 4 * i) * WAVE + lane];
-        mx = fmax(mx, fabs(x[i]));
+        const int l = (w + 4 * i) * WAVE + lane;
+        x[i] = X[l];
+        atomicMax(&bk[l < lend ? T->band_of_line[l] : PAC_NB],
+                  (unsigned long long)__double_as_longlong(fabs(x[i])));
     }
-    mx = block_max_256(mx, red);
+    __syncthreads();
+    double mx = 0.0;
+#pragma unroll
+    for (int b = 0; b <= PAC_NB; ++b) mx = fmax(mx, __longlong_as_double((long long)bk[b]));
     const int overall = pac_scale_factor(mx, 5);
     // band peak |line| of the SCALED lines: max|X| * 2^overall (exact scaling)
-    {
-        double* ax = reinterpret_cast<double*>(buf + 512);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ax[(w + 4 * i) * WAVE + lane] = fabs(x[i]);
-        __syncthreads();
-        grp_band_max(T, ax, w, lane, W.bandpeak + g * PAC_NB, 1, (double)(1 << overall), true);
-        __syncthreads();
-    }
+    if (tid < PAC_NB)
+        W.bandpeak[g * PAC_NB + tid] = T->nlines[tid] ? __longlong_as_double((long long)bk[tid]) *
+                                                            (double)(1 << overall) : 0.0;
+    __syncthreads();                       // bk read by all before the spectrum overwrites it
+    PROF_MARK(3);
 
     // --- side chain: Hann(Sine(x)) spectrum (Origin psychoac.py:223) -------
     grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf,
                                reinterpret_cast<double2*>(xs), tid);
+    PROF_MARK(4);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
+    PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     double smr[4];
 #pragma unroll 1
@@ -194,12 +221,21 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
         const double thr = wave_masking_row(buf, nm, T, lane, w + 4 * i, xs + w * 512);
         smr[i] = pac_spl(4.0 * (x[i] * x[i])) - thr;    // Origin psychoac.py:281-314
     }
+    PROF_MARK(6);
     __syncthreads();
-    double* d = reinterpret_cast<double*>(buf);
+    PROF_MARK(7);
+    // band maxima of the SMRs: atomic max on order-preserving keys of the doubles
+    unsigned long long* sk = reinterpret_cast<unsigned long long*>(buf);   // masker list is done
+    if (tid < PAC_NB) sk[tid] = 0ull;
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) d[(w + 4 * i) * WAVE + lane] = smr[i];
+    for (int i = 0; i < 4; ++i) {
+        const int l = (w + 4 * i) * WAVE + lane;
+        if (l < lend) atomicMax(&sk[T->band_of_line[l]], pac_order_key(smr[i]));
+    }
     __syncthreads();
-    grp_band_max(T, d, w, lane, W.smr + g * PAC_NB, 1, 1.0, true);
+    if (tid < PAC_NB) W.smr[g * PAC_NB + tid] = T->nlines[tid] ? pac_order_unkey(sk[tid]) : 0.0;
+    PROF_MARK(8);
     if (tid == 0) W.overall[g] = (uint8_t)overall;
 }
 
@@ -435,7 +471,7 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
     wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
-    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane);
+    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane, reinterpret_cast<int*>(tmp));
     double thr[16];
     wave_masking(buf, nm, T, lane, thr, beta);
 #pragma unroll

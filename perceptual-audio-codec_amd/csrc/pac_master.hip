@@ -47,8 +47,7 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
                                                          PacMasterWork W, int64_t gb0) {
     __shared__ double2 buf[1024];
-    __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // spectrum FFT scratch, then beta rows
-    __shared__ int cnt[16];
+    __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // FFT / peak scratch, then beta rows
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
@@ -59,7 +58,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const BlockPcm rR(locate(src, gb0 + j, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, cnt);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta));
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
 #pragma unroll 1
     for (int i = 0; i < 4; ++i) {

@@ -230,70 +230,81 @@ __device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<
 // 10 log10|X| > -30 is the equivalent |X|^2 > T->peak_floor2), masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
 // compacted masker list (ascending bin order) written over buf by a group of
-// NT threads.  cnt: LDS scratch of (1024/WAVE) ints.  Returns the masker count.
+// NT threads.  scratch: LDS of 16 + 512 ints.  Returns the masker count.
+// Peaks are compacted first (ballots, bin order = the reference's summation
+// order) so that the SPL (a log10 each) is evaluated once per masker.
 template <int NT>
 __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                double drop, int tid, int* cnt) {
+                                                double drop, int tid, int* scratch) {
     constexpr int J = 1024 / NT;
+    constexpr int NW = NT / WAVE;
+    int* cnt = scratch;              // [J][NW] peak counts of the (j, wave) segments, in bin order
+    int* kidx = scratch + 16;        // compacted peak bins
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
-    const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
-    double S[J];
+    const double floor2 = T->peak_floor2;
     unsigned long long bal[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        int k = j * NT + tid;
+        const int k = j * NT + tid;
         bool pk = false;
-        S[j] = 0.0;
         if (k >= 1 && k <= 1022) {
-            double m = buf[k].x;
-            pk = m > buf[k - 1].x && m > buf[k + 1].x && m > T->peak_floor2;
-        }
-        if (pk) {
-            double s = 0.0;
-            if (k >= 3) {
-                int hi = k + 3 < 1024 ? k + 3 : 1024;
-                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, buf[i].x);   // builtin sum, from 0
-            }
-            S[j] = pac_spl(csp * s);
+            const double m = buf[k].x;
+            pk = m > buf[k - 1].x && m > buf[k + 1].x && m > floor2;
         }
         bal[j] = __ballot(pk);
-        if (lane == 0) cnt[j * (NT / WAVE) + w] = __popcll(bal[j]);   // segment (j, w) in bin order
+        if (lane == 0) cnt[j * NW + w] = __popcll(bal[j]);
     }
-    grp_sync<NT>();   // all magnitude reads and counts done before the list overwrites buf
+    grp_sync<NT>();
+    int pre[J * NW];                 // exclusive prefix of the segment counts
     int tot = 0;
-    for (int i = 0; i < 1024 / WAVE; ++i) tot += cnt[i];
+#pragma unroll
+    for (int i = 0; i < J * NW; ++i) { pre[i] = tot; tot += cnt[i]; }
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+        if ((bal[j] >> lane) & 1ull) kidx[pre[j * NW + w] + __popcll(bal[j] & below)] = j * NT + tid;
+    grp_sync<NT>();
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    constexpr int R = (PAC_MAXMASK + NT - 1) / NT;
+    double rz[R], rB[R], rku[R], rE[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int idx = q * NT + tid;
+        if (idx < tot) {
+            const int k = kidx[idx];
+            double s = 0.0;
+            if (k >= 3) {
+                const int hi = k + 3 < 1024 ? k + 3 : 1024;
+                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, buf[i].x);   // builtin sum, from 0
+            }
+            const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
+            const double sp = pac_spl(csp * s);
+            double lev = sp - 40.0;
+            lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
+            rB[q] = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
+            rz[q] = T->bark_bin[k];
+            rku[q] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
+            rE[q] = pac_exp2(rB[q]);
+        }
+    }
+    grp_sync<NT>();   // every |X|^2 read done before the list overwrites buf
     double* mz = mk_z(buf);
     double* mB = mk_B(buf);
     double* mku = mk_ku(buf);
     double* mE = mk_E(buf);
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        if ((bal[j] >> lane) & 1ull) {
-            int base = 0;
-            const int seg = j * (NT / WAVE) + w;
-            for (int i = 0; i < seg; ++i) base += cnt[i];
-            int idx = base + __popcll(bal[j] & below);
-            int k = j * NT + tid;
-            double sp = S[j];
-            double lev = sp - 40.0;
-            lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
-            double B = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
-            mz[idx] = T->bark_bin[k];
-            mB[idx] = B;
-            mku[idx] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
-            mE[idx] = pac_exp2(B);
-        }
+    for (int q = 0; q < R; ++q) {
+        const int idx = q * NT + tid;
+        if (idx < tot) { mz[idx] = rz[q]; mB[idx] = rB[q]; mku[idx] = rku[q]; mE[idx] = rE[q]; }
     }
     grp_sync<NT>();
-    return __builtin_amdgcn_readfirstlane(tot);
+    return tot;
 }
 
 __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                 double drop, int lane) {
-    __shared__ int cnt_w[1024 / WAVE];
-    return grp_find_maskers<WAVE>(buf, T, drop, lane, cnt_w);
+                                                 double drop, int lane, int* scratch) {
+    return grp_find_maskers<WAVE>(buf, T, drop, lane, scratch);
 }
 
 // 2^(h + l) for a double-double exponent (|l| << ulp(h)): exp2(h) * (1 + l ln2)

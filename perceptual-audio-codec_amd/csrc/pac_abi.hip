@@ -130,7 +130,7 @@ static void build_tables(int fs, PacTables* t) {
         while (10.0 * log10(nextafter(m, 1.0)) <= -30.0) m = nextafter(m, 1.0);
         t->peak_floor2 = m * m;
     }
-    for (int i = 1; i < 32; i++) t->inv_int[i] = 1.0 / (double)i;
+    for (int i = 1; i < 64; i++) t->inv_int[i] = 1.0 / (double)i;
     const int step = fs / PAC_N;  // Py2 integer division, psychoac.py:188
     double mx = -1.0;
     for (int k = 0; k < PAC_HALFN; k++) {
@@ -381,7 +381,7 @@ static int report_phase_clocks(pac_ctx* c, hipStream_t s, int64_t n) {
         const long long* t = &h[g * 4 * PAC_PROF_MARKS];
         if (!t[0]) continue;
         cnt++;
-        for (int k = 1; k < PAC_PROF_MARKS; k++) {
+        for (int k = 1; k < 9; k++) {
             long long mx = 0, mn = 0;
             for (int w = 0; w < 4; w++) {
                 long long d = t[w * PAC_PROF_MARKS + k] - t[w * PAC_PROF_MARKS + k - 1];
@@ -395,8 +395,21 @@ static int report_phase_clocks(pac_ctx* c, hipStream_t s, int64_t n) {
     if (!cnt) return PAC_OK;
     fprintf(stderr, "PAC_PROF %lld workgroups, mean cycles per phase (wave mean / max-min spread):\n",
             (long long)cnt);
-    for (int k = 1; k < PAC_PROF_MARKS; k++)
+    for (int k = 1; k < 9; k++)
         fprintf(stderr, "  phase %d: %10.0f  %10.0f\n", k, mean[k] / cnt, spread[k] / cnt);
+    // masking rows: wave w, i-th row (end of previous row or mark 5 to mark 10+i)
+    double row[4][4] = {{0}};
+    for (int64_t g = 0; g < PAC_PROF_WG; g++) {
+        const long long* t = &h[g * 4 * PAC_PROF_MARKS];
+        if (!t[0]) continue;
+        for (int w = 0; w < 4; w++)
+            for (int i = 0; i < 4; i++)
+                row[w][i] += (double)(t[w * PAC_PROF_MARKS + 10 + i] -
+                                      t[w * PAC_PROF_MARKS + (i ? 9 + i : 5)]);
+    }
+    for (int w = 0; w < 4; w++)
+        fprintf(stderr, "  wave %d rows: %9.0f %9.0f %9.0f %9.0f\n", w, row[w][0] / cnt, row[w][1] / cnt,
+                row[w][2] / cnt, row[w][3] / cnt);
     return PAC_OK;
 }
 

@@ -38,7 +38,7 @@ struct PacTables {
     // findpeaks floor 10 log10|X| > -30 (psychoac.py:168) as |X|^2 > peak_floor2:
     // the square of the largest double m with 10*log10(m) <= -30 (host libm)
     double peak_floor2;
-    double inv_int[32];           // 1/i (inv_int[0] unused)
+    double inv_int[64];           // 1/i (inv_int[0] unused)
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

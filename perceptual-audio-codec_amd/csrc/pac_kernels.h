@@ -15,7 +15,7 @@ struct PacSource {
 };
 
 #define PAC_PROF_WG 4096       // workgroups sampled by the phase clocks
-#define PAC_PROF_MARKS 10
+#define PAC_PROF_MARKS 16   // 0..8 phase marks, 10..13 end of each masking row
 
 // Per-channel-block work arrays, index [g * 25 + band]: a workgroup writes
 // its channel-block's bands as one contiguous run.

@@ -142,6 +142,9 @@ __device__ __forceinline__ void grp_band_max(const PacTables* __restrict__ T, co
     }
 }
 
+// MDCT rows (64 lines) whose lines wave w of the front kernel holds
+__device__ __forceinline__ int front_row(int i, int w) { return 4 * i + w; }
+
 // unsigned keys that order like the doubles (for LDS atomic max)
 __device__ __forceinline__ unsigned long long pac_order_key(double v) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -160,8 +163,8 @@ __device__ __forceinline__ double pac_order_unkey(unsigned long long k) {
 
 // One 256-thread workgroup per channel-block.  The block is windowed once
 // into LDS; the MDCT runs first (lines kept in registers, band peaks taken),
-// then the Hann spectrum whose masker list the four waves share; each wave
-// sweeps the masking sum for rows w, w+4, w+8, w+12.
+// then the Hann spectrum whose masker list the four waves share; the waves
+// claim the 16 masking rows of 64 lines dynamically.
 __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int l = (w + 4 * i) * WAVE + lane;
+        const int l = front_row(i, w) * WAVE + lane;
         x[i] = X[l];
         atomicMax(&bk[l < lend ? T->band_of_line[l] : PAC_NB],
                   (unsigned long long)__double_as_longlong(fabs(x[i])));
@@ -215,23 +218,53 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
     PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
-    double smr[4];
+    // Masking rows are claimed dynamically, most expensive first (the order
+    // measured on broadband input: middle rows carry the most maskers on both
+    // sides); a wave keeps its (row, threshold) pairs in registers, at most 4.
+    int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));   // slot the list never uses
+    if (tid == 0) *rowctr = 0;
+    __syncthreads();
+    constexpr unsigned long long kRowOrder = 0xf0e1dc4528b9a763ull;
+    double tv0 = 0.0, tv1 = 0.0, tv2 = 0.0, tv3 = 0.0;
+    int rids = 0;                          // claimed rows, 4 bits each (wave-uniform)
+    int nr = 0;
 #pragma unroll 1
-    for (int i = 0; i < 4; ++i) {
-        const double thr = wave_masking_row(buf, nm, T, lane, w + 4 * i, xs + w * 512);
-        smr[i] = pac_spl(4.0 * (x[i] * x[i])) - thr;    // Origin psychoac.py:281-314
+    while (nr < 4) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(rowctr, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k >= 16) break;
+        const int r = (int)((kRowOrder >> (4 * k)) & 15);
+        const double thr = wave_masking_row(buf, nm, T, lane, r, xs + w * 512);
+        switch (nr) {
+            case 0: tv0 = thr; break;
+            case 1: tv1 = thr; break;
+            case 2: tv2 = thr; break;
+            default: tv3 = thr; break;
+        }
+        rids |= r << (4 * nr);
+        PROF_MARK(10 + nr);
+        ++nr;
     }
     PROF_MARK(6);
     __syncthreads();
     PROF_MARK(7);
-    // band maxima of the SMRs: atomic max on order-preserving keys of the doubles
-    unsigned long long* sk = reinterpret_cast<unsigned long long*>(buf);   // masker list is done
+    double* thr_l = reinterpret_cast<double*>(buf);        // masker list is done
+    if (nr > 0) thr_l[(rids & 15) * WAVE + lane] = tv0;
+    if (nr > 1) thr_l[((rids >> 4) & 15) * WAVE + lane] = tv1;
+    if (nr > 2) thr_l[((rids >> 8) & 15) * WAVE + lane] = tv2;
+    if (nr > 3) thr_l[((rids >> 12) & 15) * WAVE + lane] = tv3;
+    __syncthreads();
+    // SMR (Origin psychoac.py:281-314) and its band maxima: atomic max on
+    // order-preserving keys of the doubles
+    unsigned long long* sk = reinterpret_cast<unsigned long long*>(buf + 512);
     if (tid < PAC_NB) sk[tid] = 0ull;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int l = (w + 4 * i) * WAVE + lane;
-        if (l < lend) atomicMax(&sk[T->band_of_line[l]], pac_order_key(smr[i]));
+        const int l = front_row(i, w) * WAVE + lane;
+        const double smr = pac_spl(4.0 * (x[i] * x[i])) - thr_l[l];
+        if (l < lend) atomicMax(&sk[T->band_of_line[l]], pac_order_key(smr));
     }
     __syncthreads();
     if (tid < PAC_NB) W.smr[g * PAC_NB + tid] = T->nlines[tid] ? pac_order_unkey(sk[tid]) : 0.0;

@@ -29,6 +29,48 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
+// Cross-lane moves of a double through DPP (VALU, no LDS round trip).  Lanes
+// outside ROWMASK (or without a source) get `old`.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double old, double v) {
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, ROWMASK, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+#define PAC_DPP_QXOR1 0xB1     // quad_perm [1,0,3,2]
+#define PAC_DPP_QXOR2 0x4E     // quad_perm [2,3,0,1]
+#define PAC_DPP_HMIRROR 0x141  // row_half_mirror
+#define PAC_DPP_MIRROR 0x140   // row_mirror
+#define PAC_DPP_BCAST15 0x142
+#define PAC_DPP_BCAST31 0x143
+// Wave-wide reductions (wave-uniform result; the same value on every lane)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    v += dpp_f64<PAC_DPP_QXOR1>(0.0, v);
+    v += dpp_f64<PAC_DPP_QXOR2>(0.0, v);
+    v += dpp_f64<PAC_DPP_HMIRROR>(0.0, v);
+    v += dpp_f64<PAC_DPP_MIRROR>(0.0, v);              // row sums
+    v += dpp_f64<PAC_DPP_BCAST15, 0xa>(0.0, v);        // rows 1, 3 += rows 0, 2
+    v += dpp_f64<PAC_DPP_BCAST31, 0xc>(0.0, v);        // rows 2, 3 += rows 0 + 1
+    return readlane_f64(v, 63);
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_ext_f64(double v) {
+    auto f = [](double a, double b) { return MAX ? fmax(a, b) : fmin(a, b); };
+    v = f(v, dpp_f64<PAC_DPP_QXOR1>(v, v));
+    v = f(v, dpp_f64<PAC_DPP_QXOR2>(v, v));
+    v = f(v, dpp_f64<PAC_DPP_HMIRROR>(v, v));
+    v = f(v, dpp_f64<PAC_DPP_MIRROR>(v, v));
+    v = f(v, dpp_f64<PAC_DPP_BCAST15, 0xa>(v, v));
+    v = f(v, dpp_f64<PAC_DPP_BCAST31, 0xc>(v, v));
+    return readlane_f64(v, 63);
+}
+
 __device__ __forceinline__ unsigned brev(unsigned x, int bits) {
     return __builtin_bitreverse32(x) >> (32 - bits);
 }
@@ -219,7 +261,7 @@ __device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* 
 #define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
 #define PAC_LN2 0.6931471805599453
 #define PAC_MOM_MIN 24      // fewest common upper maskers for the moment form
-#define PAC_MOM_DMAX 24     // highest Taylor degree of the moment form
+#define PAC_MOM_DMAX 40     // highest Taylor degree of the moment form
 
 __device__ __forceinline__ double* mk_z(double2* buf) { return reinterpret_cast<double*>(buf); }
 __device__ __forceinline__ double* mk_B(double2* buf) { return reinterpret_cast<double*>(buf) + 512; }
@@ -416,9 +458,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
     }
     // --- upper side, ascending
     const double tiq = T->tiq[l];
-    double lb = tiq + flat + lower;                       // I(l) >= lb
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { double w = __shfl_xor(lb, o, WAVE); lb = w < lb ? w : lb; }
+    const double lb = wave_ext_f64<false>(tiq + flat + lower);   // I(l) >= lb on every lane
     // floor(log2 lb) - 64 from the exponent field: a conservative cut
     const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
     int m0 = umax;                    // first masker that is not negligible (64 tested at once)
@@ -454,19 +494,16 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
             kmn = fmin(kmn, k);
             kmx = fmax(kmx, k);
         }
-        double adl = fabs(dl);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            kmn = fmin(kmn, __shfl_xor(kmn, o, WAVE));
-            kmx = fmax(kmx, __shfl_xor(kmx, o, WAVE));
-            adl = fmax(adl, __shfl_xor(adl, o, WAVE));
-        }
+        kmn = wave_ext_f64<false>(kmn);
+        kmx = wave_ext_f64<true>(kmx);
+        // max |z_l - z_mid| over the row (ascending z: an end line)
+        const double adl = fmax(zm - zr, T->bark_line[r * WAVE + WAVE - 1] - zm);
         const double kc = 0.5 * (kmn + kmx);
         const double eps = (0.5 * (kmx - kmn) * adl) * PAC_LN2 * 1.0000001;
-        // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57
+        // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57 (uniform)
         int D = 0;
         double rem = pac_exp2(eps * 1.4426950408889634) * eps;  // e^eps eps^1/1!
-        while (rem > 0x1p-57 && D < PAC_MOM_DMAX + 1) { ++D; rem *= eps / (double)(D + 1); }
+        while (rem > 0x1p-57 && D < PAC_MOM_DMAX + 1) { ++D; rem *= eps * T->inv_int[D + 1]; }
         D = __builtin_amdgcn_readfirstlane(D);
         if (D <= PAC_MOM_DMAX) {
             direct = false;
@@ -480,9 +517,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
                     part += p;
                     beta[m] = p * (mku[m] - kc);
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, WAVE);
-                acc = __builtin_fma(part, q, acc);
+                acc = __builtin_fma(wave_sum_f64(part), q, acc);
                 q = (q * x) * T->inv_int[d + 1];
             }
             up = acc * pac_exp2(kc * dl);

@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpacgpu.so")
+LIB_PATH = os.environ.get("PAC_LIB") or os.path.join(HERE, "libpacgpu.so")   # PAC_LIB: A/B builds
 HUFF_PATH = os.path.join(HERE, "data", "huffman_tables.bin")
 
 PAC_OK = 0

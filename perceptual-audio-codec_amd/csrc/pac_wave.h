@@ -524,7 +524,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
         }
     }
     if (direct) {
-#pragma unroll 4
+#pragma unroll 2
         for (int m = m0; m < ua; ++m)               // m < umin <= U on every lane
             up += pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
     }

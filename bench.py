@@ -89,6 +89,30 @@ class Dist:
             self.td.destroy_process_group()
 
 
+# the reference's direct masking sum costs ~35 FP64
+# flops per (masker, line) pair, ~2 x 255 x 1024 pairs per stereo block for
+# the origin coder -> ~18 MFLOP per block.  Our kernel evaluates the same sum
+# in factored forms; "ref_alg_equiv_tflops" prices our rate at
+# the reference algorithm's flop count.
+REF_ALG_FLOP_PER_BLOCK = 18.0e6
+
+
+def measured_profile():
+    """Per-block HBM bytes and FP64 work of k_origin_front from the newest
+    committed rocprofv3 PMC summary (profiles/*_origin_pmc.json, made by
+    profiles/run_profile.sh + profiles/summarize_pmc.py on this kernel build)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_origin_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    if "k_origin_front" not in d:
+        return None
+    d["_file"] = os.path.relpath(files[-1], ROOT)
+    return d
+
+
 def cpu_baseline(ctx, dev_pcm, frames_per_stream, fs, seconds):
     """The CPU oracle (oracle/pac_oracle.c, 1 thread) on a bounded sample of
     the same workload: the first hops of stream 0, copied back from HBM."""
@@ -163,8 +187,18 @@ def main():
     front_s = float(np.mean(fronts)) / 1e3
     alg_bytes = blocks * (4096 + 2 * (25 * 8 * 2 + 1))
     achieved = alg_bytes / front_s / 1e9
-    # FP64 work of the masking sum: ~20 fp64 VALU ops per masker-line pair is
-    # measured by PMC (profiles/); here only report the pair count per block
+    prof = measured_profile()
+    traffic = None
+    fp64 = {"ref_alg_flop_per_block": REF_ALG_FLOP_PER_BLOCK,
+            "ref_alg_equiv_tflops": REF_ALG_FLOP_PER_BLOCK * blocks / front_s / 1e12,
+            "peak_tflops": FP64_PEAK_TFLOPS}
+    if prof:
+        f = prof["k_origin_front"]
+        traffic = (f["hbm_read_bytes_per_block"] + f["hbm_write_bytes_per_block"]) * blocks
+        fp64.update({"executed_flop_per_block": f["fp64_flop_per_block"],
+                     "executed_tflops": f["fp64_flop_per_block"] * blocks / front_s / 1e12,
+                     "executed_frac": f["fp64_flop_per_block"] * blocks / front_s / 1e12 / FP64_PEAK_TFLOPS,
+                     "valu_issue_util": f["valu_issue_util"], "source": prof["_file"]})
     res = {
         "metric": "stereo 1024-sample blocks encoded/s",
         "value": value,
@@ -187,8 +221,11 @@ def main():
                    % dist.world},
         "roofline": {"bound": "hbm", "kernel": "k_origin_front", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None,
-                     "note": "path is FP64-VALU bound (masking sum), see DESIGN.md"},
+                     "traffic": traffic,
+                     "traffic_source": prof["_file"] if prof else None,
+                     "note": "k_origin_front is FP64-VALU bound (masking sum), not HBM bound: "
+                             "see 'fp64' and DESIGN.md section 4"},
+        "fp64": fp64,
         "kernels_ms": {"front": float(np.mean(fronts)), "alloc": float(np.mean(alloc_ms)),
                        "pack": float(np.mean(pack_ms)), "step_device": float(np.mean(totals))},
         "out_bytes_per_gpu": out_bytes,

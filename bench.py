@@ -42,13 +42,22 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=1000)
+    ap.add_argument("--profile", choices=["origin", "master"], default="origin",
+                    help="origin = BASELINE configs[1] (white noise, M/S off, the metric's config); "
+                         "master = configs[2] (pink noise + tones, M/S + Huffman)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="default 1000 (origin, 10^6 blocks) / 10000 (master, 10^7 blocks)")
     ap.add_argument("--blocks-per-stream", type=int, default=1000)
     ap.add_argument("--sample-rate", type=int, default=48000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (oracle on host cores)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads of the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.streams is None:
+        a.streams = 10000 if a.profile == "master" else 1000
+    return a
 
 
 class Dist:
@@ -95,6 +104,7 @@ class Dist:
 # in factored forms; "ref_alg_equiv_tflops" prices our rate at
 # the reference algorithm's flop count.
 REF_ALG_FLOP_PER_BLOCK = 18.0e6
+REF_ALG_FLOP_PER_BLOCK_MASTER = 48.0e6     # 6 thresholds x ~222 maskers x 1024 lines
 
 
 def measured_profile():
@@ -113,45 +123,62 @@ def measured_profile():
     return d
 
 
-def cpu_baseline(ctx, dev_pcm, frames_per_stream, fs, seconds):
-    """The CPU oracle (oracle/pac_oracle.c, 1 thread) on a bounded sample of
-    the same workload: the first hops of stream 0, copied back from HBM."""
+def cpu_baseline(ctx, dev_pcm, frames_per_stream, n_streams, fs, seconds, profile, threads):
+    """The CPU oracle (oracle/pac_oracle.c) on a bounded sample of the same
+    workload, one host thread per stream (ctypes releases the GIL; the C
+    oracle keeps no global state): thread t encodes growing prefixes of stream
+    t, copied back from HBM, until `seconds` have passed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as P
+    from concurrent.futures import ThreadPoolExecutor
     P.lib()
+    threads = max(1, min(threads, n_streams))
     hops = min(frames_per_stream // 1024, 4096)
-    pcm = np.empty((hops * 1024, 2), dtype=np.int16)
-    ctx.to_host(pcm, dev_pcm)
-    o = P.Oracle(fs, huffman=False)
-    done, t0, chunk = 0, time.perf_counter(), 16
-    while True:
-        n = min(chunk, hops - 1)
-        o.encode_data(P.ORIGIN, pcm[: n * 1024], max_blocks=n)
-        done += n
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= 200000:
-            break
-        chunk = min(chunk * 2, hops - 1)
-    return {"value": done / el, "unit": "blocks/s", "cores": 1, "kind": "port",
+    pcms = []
+    for t in range(threads):
+        pcm = np.empty((hops * 1024, 2), dtype=np.int16)
+        ctx.to_host(pcm, dev_pcm + t * frames_per_stream * 4)
+        pcms.append(pcm)
+    prof = P.MASTER if profile == "master" else P.ORIGIN
+    t0 = time.perf_counter()
+
+    def work(t):
+        o = P.Oracle(fs, huffman=(prof == P.MASTER))
+        done, chunk = 0, 16
+        while time.perf_counter() - t0 < seconds and done < 200000:
+            n = min(chunk, hops - 1)
+            o.encode_data(prof, pcms[t][: n * 1024], max_blocks=n)
+            done += n
+            chunk = min(chunk * 2, hops - 1)
+        return done
+
+    with ThreadPoolExecutor(threads) as ex:
+        done = sum(ex.map(work, range(threads)))
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
-                      "fixtures), 1 host thread, %d stereo blocks of the same synthetic "
-                      "48 kHz white-noise stream in %.1f s" % (done, el)}
+                      "fixtures), %s profile, %d host threads (one stream each), %d stereo "
+                      "blocks of the same synthetic streams in %.1f s" % (profile, threads, done, el)}
 
 
 def main():
     a = parse()
     dist = Dist()
-    ctx = _lib.Context(dist.local, huffman=False)
+    master = a.profile == "master"
+    ctx = _lib.Context(dist.local, huffman=master)
     fs = a.sample_rate
     hops = a.blocks_per_stream - 1
     fps = hops * 1024
     ns = a.streams
     n_frames = ns * fps
     fo = np.arange(ns + 1, dtype=np.int64) * fps
-    p = _lib.params(fs, 2, 0)
+    p = _lib.params(fs, 2, 1 if master else 0)
     blocks = ns * a.blocks_per_stream
     pcm_dev = ctx.alloc(n_frames * 2 * 2)
-    ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * dist.rank)
+    if master:
+        ctx.synth_pink_tones(pcm_dev, n_frames, fs, seed=1234 + 7919 * dist.rank)
+    else:
+        ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * dist.rank)
     cap = int(ctx.L.pac_encode_bound(C.byref(p), ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
     out_dev = ctx.alloc(cap)
     ctx.set_timing(True)
@@ -181,16 +208,21 @@ def main():
     total_blocks = dist.sum(blocks)
     value = total_blocks / (el_max / a.steps)
 
-    # roofline of the dominant kernel (k_origin_front): algorithmic bytes per
-    # launch = int16 PCM read (4096 B per stereo block) + SMR/peak/scale
-    # outputs (2 x (25*8 + 25*8 + 1) B per stereo block)
+    # roofline of the dominant kernel.  origin: k_origin_front, algorithmic
+    # bytes per launch = int16 PCM read (4096 B per stereo block) + SMR/peak/
+    # scale outputs (2 x (25*8 + 25*8 + 1) B per stereo block).  master: the
+    # front time covers k_master_thr + k_master_front; k_master_thr reads the
+    # PCM (4096 B) and writes the 6 thresholds (6 x 1024 x 8 B) per block.
     front_s = float(np.mean(fronts)) / 1e3
-    alg_bytes = blocks * (4096 + 2 * (25 * 8 * 2 + 1))
+    kern = "k_master_thr" if master else "k_origin_front"
+    per_block = 4096 + (6 * 1024 * 8 if master else 2 * (25 * 8 * 2 + 1))
+    alg_bytes = blocks * per_block
     achieved = alg_bytes / front_s / 1e9
-    prof = measured_profile()
+    prof = None if master else measured_profile()
     traffic = None
-    fp64 = {"ref_alg_flop_per_block": REF_ALG_FLOP_PER_BLOCK,
-            "ref_alg_equiv_tflops": REF_ALG_FLOP_PER_BLOCK * blocks / front_s / 1e12,
+    ref_flop = REF_ALG_FLOP_PER_BLOCK_MASTER if master else REF_ALG_FLOP_PER_BLOCK
+    fp64 = {"ref_alg_flop_per_block": ref_flop,
+            "ref_alg_equiv_tflops": ref_flop * blocks / front_s / 1e12,
             "peak_tflops": FP64_PEAK_TFLOPS}
     if prof:
         f = prof["k_origin_front"]
@@ -199,6 +231,15 @@ def main():
                      "executed_tflops": f["fp64_flop_per_block"] * blocks / front_s / 1e12,
                      "executed_frac": f["fp64_flop_per_block"] * blocks / front_s / 1e12 / FP64_PEAK_TFLOPS,
                      "valu_issue_util": f["valu_issue_util"], "source": prof["_file"]})
+    if master:
+        data = "synthetic (device-generated pink noise (Voss, counter hash) + 440/1250/5300 Hz tones)"
+        workload = ("BASELINE configs[2]: synthetic 48 kHz stereo pink noise + tones, %d stereo "
+                    "blocks per GPU, N=1024 MDCT, full psychoacoustics + M/S + bit allocation + "
+                    "Huffman (master profile)" % blocks)
+    else:
+        data = "synthetic (device-generated white noise, counter-hash Box-Muller)"
+        workload = ("BASELINE configs[1]: synthetic 48 kHz stereo white noise, 10^6 stereo blocks "
+                    "per GPU, N=1024 MDCT, M/S off (origin profile)")
     res = {
         "metric": "stereo 1024-sample blocks encoded/s",
         "value": value,
@@ -211,27 +252,26 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (device-generated white noise, counter-hash Box-Muller)",
-        "config": {"workload": "BASELINE configs[1]: synthetic 48 kHz stereo white noise, "
-                               "10^6 stereo blocks per GPU, N=1024 MDCT, M/S off "
-                               "(origin profile)",
-                   "profile": "origin", "sample_rate": fs, "streams_per_gpu": ns,
+        "data": data,
+        "config": {"workload": workload,
+                   "profile": a.profile, "sample_rate": fs, "streams_per_gpu": ns,
                    "blocks_per_stream": a.blocks_per_stream,
                    "global_blocks": int(total_blocks), "parallelism": "streams sharded, %d rank(s)"
                    % dist.world},
-        "roofline": {"bound": "hbm", "kernel": "k_origin_front", "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": kern, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
                      "traffic_source": prof["_file"] if prof else None,
-                     "note": "k_origin_front is FP64-VALU bound (masking sum), not HBM bound: "
-                             "see 'fp64' and DESIGN.md section 4"},
+                     "note": "%s is FP64-VALU bound (masking sum), not HBM bound: "
+                             "see 'fp64' and DESIGN.md section 4" % kern},
         "fp64": fp64,
         "kernels_ms": {"front": float(np.mean(fronts)), "alloc": float(np.mean(alloc_ms)),
                        "pack": float(np.mean(pack_ms)), "step_device": float(np.mean(totals))},
         "out_bytes_per_gpu": out_bytes,
     }
     if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(ctx, pcm_dev, fps, fs, a.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(ctx, pcm_dev, fps, ns, fs, a.cpu_seconds, a.profile,
+                                           a.cpu_threads)
     ctx.free(out_dev)
     ctx.free(pcm_dev)
     if dist.rank == 0:

@@ -127,6 +127,10 @@ int pac_copy_to_device(pac_ctx *ctx, void *dst, const void *src, int64_t bytes);
 int pac_copy_to_host(pac_ctx *ctx, void *dst, const void *src, int64_t bytes);
 /* Synthetic 48 kHz-style white-noise PCM: N(0,1)*0.25*32767, rint, clip. */
 int pac_synth_white(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_samples, uint64_t seed);
+/* Synthetic stereo pink noise + 440/1250/5300 Hz tones (BASELINE configs[2]),
+ * n_frames interleaved L/R frames. */
+int pac_synth_pink_tones(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_frames, int32_t sample_rate,
+                         uint64_t seed);
 int pac_sync(pac_ctx *ctx);
 int pac_set_timing(pac_ctx *ctx, int32_t enable);
 /* Stereo blocks per master-profile chunk (device scratch ~65 KB/block). */

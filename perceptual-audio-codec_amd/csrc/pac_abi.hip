@@ -197,7 +197,9 @@ struct pac_ctx {
     // master
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
-    DevBuf<int64_t> st_extra, st_deposit, base;
+    DevBuf<int64_t> st_extra, st_deposit, st_cursor, m_src_off, m_dst_off, m_size;
+    DevBuf<uint8_t> m_stage;                // master: packed bytes of a stream group before the copy
+    int64_t stage_max = (int64_t)16 << 30;  // bytes of worst-case output per stream group
     PacHuffTables* huff_host = nullptr;
     std::unordered_map<uint64_t, int> huff_dec[PAC_NTAB];   // (len<<32|code) -> symbol, -1 = escape
     int64_t chunk_blocks = 32768;
@@ -235,7 +237,8 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     free(c->huff_host);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
-    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->base.release();
+    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->st_cursor.release();
+    c->m_src_off.release(); c->m_dst_off.release(); c->m_size.release(); c->m_stage.release();
     c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release(); c->prof.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
@@ -352,13 +355,17 @@ static double bit_budget(const pac_params* p) {
     return b;
 }
 
+// worst-case bytes of one channel-block: '<L' + payload <= 4 + 25*8 + 16*1024
+// (+ 25 LRMS + sign bits + escape codes for master) bits
+static int64_t pac_encode_bound_per_channel_block() {
+    return 4 + (4 + 4 + 25 * 8 + 16 * 1024 + 25 + 1024 + 1024 * 16 + 7) / 8;
+}
+
 extern "C" int64_t pac_encode_bound(const pac_params* p, int32_t n_streams, const int64_t* fo) {
     if (!p || !fo || n_streams < 0) return -1;
     int64_t blocks = 0;
     for (int s = 0; s < n_streams; s++) blocks += (fo[s + 1] - fo[s] + PAC_HALFN - 1) / PAC_HALFN + 1;
-    // payload <= 4 + 25*8 + 16*1024 (+ 25 LRMS + sign bits for master) bits
-    int64_t per = 4 + (4 + 4 + 25 * 8 + 16 * 1024 + 25 + 1024 + 1024 * 16 + 7) / 8;
-    return blocks * p->n_channels * per;
+    return blocks * p->n_channels * pac_encode_bound_per_channel_block();
 }
 
 __global__ void k_stream_offsets(const int64_t* __restrict__ off, const int64_t* __restrict__ blk_off,
@@ -474,92 +481,135 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
 
 // Runs the master pipeline over global blocks [0, nblocks).  States (device
 // st_extra / st_deposit, per stream) must be initialised by the caller.
+// Master profile.  Streams are taken in groups whose worst-case output fits
+// the staging area (c->stage_max) and whose size is at most c->chunk_blocks;
+// each group is swept in time slices of S blocks per stream (S * streams <=
+// chunk_blocks), so every stream's serial reservoir chain advances in
+// parallel.  Packed channel-blocks land in staging at each stream's running
+// cursor; after the group, k_copy_streams moves every stream to its final
+// offset.  Fills c->stream_off (n_streams + 1 entries) on the device.
 static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src,
                       const std::vector<int64_t>& blk, uint8_t* out_dev, int64_t out_cap,
                       int64_t* out_total) {
     int rc;
     const int n_streams = src.n_streams;
-    const int64_t nblocks = blk[n_streams];
-    const int64_t CB = c->chunk_blocks;
-    const int64_t cb = nblocks < CB ? nblocks : CB;
-    if ((rc = c->m_thr.ensure(cb * 6 * PAC_HALFN)) || (rc = c->m_lines.ensure(cb * 2 * PAC_HALFN)) ||
-        (rc = c->m_smr.ensure(cb * 2 * PAC_NB)) || (rc = c->m_peak.ensure(cb * 2 * PAC_NB)) ||
-        (rc = c->m_lrms.ensure(cb * PAC_NB)) || (rc = c->m_overall.ensure(cb * 2)) ||
-        (rc = c->m_ba.ensure(cb * 2 * PAC_NB)) || (rc = c->m_sf.ensure(cb * 2 * PAC_NB)) ||
-        (rc = c->m_tid.ensure(cb * 2)) || (rc = c->nbytes.ensure(cb * 2)) ||
-        (rc = c->off.ensure(cb * 2 + 1)) ||
-        (rc = c->tile_sums.ensure((cb * 2 + SCAN_TILE - 1) / SCAN_TILE + 1)) ||
-        (rc = c->grand_total.ensure(1)) || (rc = c->base.ensure(1)))
+    const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : 1;
+    const int64_t per = pac_encode_bound_per_channel_block();
+    std::vector<int64_t> lens(n_streams);
+    int64_t maxlen = 0;
+    for (int s = 0; s < n_streams; s++) {
+        lens[s] = blk[s + 1] - blk[s];
+        if (lens[s] > maxlen) maxlen = lens[s];
+    }
+    if ((rc = c->st_cursor.ensure(n_streams)) || (rc = c->m_src_off.ensure(n_streams)) ||
+        (rc = c->m_dst_off.ensure(n_streams)) || (rc = c->m_size.ensure(n_streams)))
         return rc;
-    PacMasterWork W{c->m_thr.p, c->m_lines.p, c->m_smr.p, c->m_peak.p, c->m_lrms.p, c->m_overall.p,
-                    c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p};
     hipStream_t s = c->stream;
     const double budget = bit_budget(p);
-    HIPCHK(hipMemsetAsync(c->base.p, 0, sizeof(int64_t), s));
-    float t_front = 0, t_alloc = 0, t_scan = 0, t_pack = 0;
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
-    for (int64_t gb0 = 0; gb0 < nblocks; gb0 += CB) {
-        const int64_t gb1 = gb0 + CB < nblocks ? gb0 + CB : nblocks;
-        const int64_t B = gb1 - gb0, G = 2 * B;
-        int s_first = (int)(std::upper_bound(blk.begin(), blk.end(), gb0) - blk.begin()) - 1;
-        int s_last = (int)(std::upper_bound(blk.begin(), blk.end(), gb1 - 1) - blk.begin()) - 1;
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
-        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, gb0);
-        hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(64), 0, s, src, T, W, gb0);
-        HIPCHK(hipGetLastError());
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
-        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)(s_last - s_first + 1)), dim3(64), 0, s, T, c->huff,
-                           W, c->blk_off.p, s_first, gb0, gb1, c->st_extra.p, c->st_deposit.p, budget);
-        HIPCHK(hipGetLastError());
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
-        int64_t ntiles = (G + SCAN_TILE - 1) / SCAN_TILE;
-        hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G, c->tile_sums.p);
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tile_sums.p, ntiles, c->grand_total.p);
-        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(256), 0, s, c->nbytes.p, G,
-                           c->tile_sums.p, c->off.p);
-        int64_t base = 0, tot = 0;
-        HIPCHK(hipMemcpyAsync(&base, c->base.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(&tot, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    float t_front = 0, t_alloc = 0, t_copy = 0, t_pack = 0;
+    std::vector<int64_t> so(n_streams + 1, 0), src_off(n_streams), cursor(n_streams), dst(n_streams),
+        size(n_streams);
+    int64_t total = 0;
+    for (int g0 = 0; g0 < n_streams;) {
+        // --- the group [g0, g1)
+        int64_t bound = 0, gmax = 0;
+        int g1 = g0;
+        while (g1 < n_streams) {
+            const int64_t b = lens[g1] * 2 * per;
+            if (g1 > g0 && (bound + b > c->stage_max || (int64_t)(g1 - g0) >= CB)) break;
+            src_off[g1] = bound;
+            bound += b;
+            if (lens[g1] > gmax) gmax = lens[g1];
+            g1++;
+        }
+        const int n_s = g1 - g0;
+        // slice length: S blocks of each stream per chunk, never past the longest
+        int64_t S64 = CB / n_s;
+        if (S64 > gmax) S64 = gmax;
+        if (S64 < 1) S64 = 1;
+        const int S = (int)S64;
+        const int64_t cb = (int64_t)n_s * S;          // local blocks per chunk
+        HIPCHK(hipStreamSynchronize(s));              // nothing in flight before any re-allocation
+        if ((rc = c->m_stage.ensure(bound > 0 ? bound : 1)) || (rc = c->m_thr.ensure(cb * 6 * PAC_HALFN)) ||
+            (rc = c->m_lines.ensure(cb * 2 * PAC_HALFN)) || (rc = c->m_smr.ensure(cb * 2 * PAC_NB)) ||
+            (rc = c->m_peak.ensure(cb * 2 * PAC_NB)) || (rc = c->m_lrms.ensure(cb * PAC_NB)) ||
+            (rc = c->m_overall.ensure(cb * 2)) || (rc = c->m_ba.ensure(cb * 2 * PAC_NB)) ||
+            (rc = c->m_sf.ensure(cb * 2 * PAC_NB)) || (rc = c->m_tid.ensure(cb * 2)) ||
+            (rc = c->nbytes.ensure(cb * 2)) || (rc = c->off.ensure(cb * 2 + 1)))
+            return rc;
+        const PacMasterWork W{c->m_thr.p, c->m_lines.p, c->m_smr.p, c->m_peak.p, c->m_lrms.p, c->m_overall.p,
+                              c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p};
+        HIPCHK(hipMemcpyAsync(c->st_cursor.p + g0, src_off.data() + g0, n_s * sizeof(int64_t),
+                              hipMemcpyHostToDevice, s));
+        for (int64_t t0 = 0; t0 < gmax; t0 += S) {
+            const PacMasterChunk ck{g0, n_s, t0, S};
+            const int64_t B = (int64_t)n_s * S;
+            if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, ck);
+            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(64), 0, s, src, T, W, ck);
+            HIPCHK(hipGetLastError());
+            if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
+            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)n_s), dim3(64), 0, s, T, c->huff, W, c->blk_off.p, ck,
+                               c->st_extra.p, c->st_deposit.p, c->st_cursor.p, c->off.p, budget);
+            HIPCHK(hipGetLastError());
+            if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
+            hipLaunchKernelGGL(k_master_pack, dim3((unsigned)(2 * B)), dim3(64), 0, s, T, c->huff, W,
+                               c->blk_off.p, ck, c->off.p, c->m_stage.p);
+            HIPCHK(hipGetLastError());
+            if (c->timing) {
+                HIPCHK(hipEventRecord(c->ev[4], s));
+                HIPCHK(hipEventSynchronize(c->ev[4]));
+                float a, b2, d;
+                hipEventElapsedTime(&a, c->ev[1], c->ev[2]);
+                hipEventElapsedTime(&b2, c->ev[2], c->ev[3]);
+                hipEventElapsedTime(&d, c->ev[3], c->ev[4]);
+                t_front += a; t_alloc += b2; t_pack += d;
+            }
+        }
+        // --- final offsets of the group's streams, then the copy
+        HIPCHK(hipMemcpyAsync(cursor.data() + g0, c->st_cursor.p + g0, n_s * sizeof(int64_t),
+                              hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (base + tot > out_cap)
-            return set_err(PAC_E_CAPACITY, "output needs > %lld bytes, capacity %lld",
-                           (long long)(base + tot), (long long)out_cap);
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[4], s));
-        hipLaunchKernelGGL(k_master_pack, dim3((unsigned)G), dim3(64), 0, s, T, c->huff, W, c->off.p,
-                           c->base.p, out_dev);
-        hipLaunchKernelGGL(k_master_stream_offsets, dim3((n_streams + 255) / 256), dim3(256), 0, s, c->off.p,
-                           c->blk_off.p, n_streams, gb0, gb1, c->base.p, c->stream_off.p);
-        hipLaunchKernelGGL(k_add_base, dim3(1), dim3(64), 0, s, c->base.p, c->grand_total.p);
+        for (int k = g0; k < g1; k++) {
+            size[k] = cursor[k] - src_off[k];
+            dst[k] = total;
+            so[k] = total;
+            total += size[k];
+        }
+        if (total > out_cap)
+            return set_err(PAC_E_CAPACITY, "output needs > %lld bytes, capacity %lld", (long long)total,
+                           (long long)out_cap);
+        HIPCHK(hipMemcpyAsync(c->m_src_off.p + g0, src_off.data() + g0, n_s * sizeof(int64_t),
+                              hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->m_dst_off.p + g0, dst.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->m_size.p + g0, size.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+        hipLaunchKernelGGL(k_copy_streams, dim3((unsigned)n_s), dim3(256), 0, s, c->m_stage.p, c->m_src_off.p + g0,
+                           c->m_dst_off.p + g0, c->m_size.p + g0, out_dev);
         HIPCHK(hipGetLastError());
         if (c->timing) {
-            HIPCHK(hipEventRecord(c->ev[0], s));   // reuse as chunk end
-            HIPCHK(hipEventSynchronize(c->ev[0]));
-            float a, b2, c3, d;
+            HIPCHK(hipEventRecord(c->ev[2], s));
+            HIPCHK(hipEventSynchronize(c->ev[2]));
+            float a;
             hipEventElapsedTime(&a, c->ev[1], c->ev[2]);
-            hipEventElapsedTime(&b2, c->ev[2], c->ev[3]);
-            hipEventElapsedTime(&c3, c->ev[3], c->ev[4]);
-            hipEventElapsedTime(&d, c->ev[4], c->ev[0]);
-            t_front += a; t_alloc += b2; t_scan += c3; t_pack += d;
+            t_copy += a;
         }
+        g0 = g1;
     }
-    int64_t total = 0;
-    HIPCHK(hipMemcpyAsync(&total, c->base.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    so[n_streams] = total;
+    HIPCHK(hipMemcpyAsync(c->stream_off.p, so.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     if (c->timing) {
         c->last.front_ms = t_front;
         c->last.alloc_ms = t_alloc;
-        c->last.scan_ms = t_scan;
+        c->last.scan_ms = t_copy;
         c->last.pack_ms = t_pack;
-        c->last.total_ms = t_front + t_alloc + t_scan + t_pack;
-        c->last.n_channel_blocks = 2 * nblocks;
+        c->last.total_ms = t_front + t_alloc + t_copy + t_pack;
+        c->last.n_channel_blocks = 2 * blk[n_streams];
         c->last.out_bytes = total;
     }
     *out_total = total;
     return PAC_OK;
-}
-
-__global__ void k_set_last(int64_t* __restrict__ so, int n, const int64_t* __restrict__ base) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) so[n] = *base;
 }
 
 extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_streams, const int16_t* pcm,
@@ -619,8 +669,6 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
         if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total))) return rc;
-        hipLaunchKernelGGL(k_set_last, dim3(1), dim3(64), 0, s, c->stream_off.p, n_streams, c->base.p);
-        HIPCHK(hipGetLastError());
         if (states) {
             HIPCHK(hipMemcpyAsync(ex.data(), c->st_extra.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(dp.data(), c->st_deposit.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -789,6 +837,16 @@ extern "C" int pac_synth_white(pac_ctx* c, int16_t* dev_pcm, int64_t n, uint64_t
     if (!c || !dev_pcm || n < 0) return set_err(PAC_E_ARG, "bad argument");
     HIPCHK(hipSetDevice(c->device));
     hipLaunchKernelGGL(k_synth_white, dim3(4096), dim3(256), 0, c->stream, dev_pcm, n, seed);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return PAC_OK;
+}
+extern "C" int pac_synth_pink_tones(pac_ctx* c, int16_t* dev_pcm, int64_t n_frames, int32_t sample_rate,
+                                    uint64_t seed) {
+    if (!c || !dev_pcm || n_frames < 0 || sample_rate <= 0) return set_err(PAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_synth_pink_tones, dim3(4096), dim3(256), 0, c->stream, dev_pcm, n_frames,
+                       (double)sample_rate, seed);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return PAC_OK;

@@ -224,7 +224,6 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));   // slot the list never uses
     if (tid == 0) *rowctr = 0;
     __syncthreads();
-    constexpr unsigned long long kRowOrder = 0xf0e1dc4528b9a763ull;
     double tv0 = 0.0, tv1 = 0.0, tv2 = 0.0, tv3 = 0.0;
     int rids = 0;                          // claimed rows, 4 bits each (wave-uniform)
     int nr = 0;
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
         if (lane == 0) k = atomicAdd(rowctr, 1);
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
-        const int r = (int)((kRowOrder >> (4 * k)) & 15);
+        const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
         const double thr = wave_masking_row(buf, nm, T, lane, r, xs + w * 512);
         switch (nr) {
             case 0: tv0 = thr; break;
@@ -547,5 +546,37 @@ __global__ void k_synth_white(int16_t* __restrict__ pcm, int64_t n, uint64_t see
         double v = __builtin_rint(z * 0.25 * 32767.0);
         v = v > 32767.0 ? 32767.0 : (v < -32768.0 ? -32768.0 : v);
         pcm[i] = (int16_t)v;
+    }
+}
+
+// synthetic config-3 input (bench): pink noise + tones, stereo interleaved.
+// Pink: Voss-McCartney sum of 16 octave-held uniform hashes (counter based,
+// so every sample is independent work); tones 440/1250/5300 Hz as in
+// pac_amd.synth.pink_tones_pcm.  L = 0.1 p1 + tones, R = 0.07 p1 + 0.03 p2 + 0.8 tones.
+__device__ __forceinline__ double voss_pink(uint64_t seed, int64_t i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t h = splitmix64(seed ^ ((uint64_t)k << 56) ^ (uint64_t)(i >> k));
+        acc += (double)(h >> 11) * 0x1.0p-52 - 1.0;        // uniform [-1, 1)
+    }
+    return acc * 0.4330127018922193;                          // / sqrt(16/3): unit variance
+}
+__global__ void k_synth_pink_tones(int16_t* __restrict__ pcm, int64_t n_frames, double fs, uint64_t seed) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (; i < n_frames; i += stride) {
+        const double t = (double)i / fs;
+        const double tones = 0.2 * sin(6.283185307179586 * 440.0 * t) +
+                             0.1 * sin(6.283185307179586 * 1250.0 * t) +
+                             0.05 * sin(6.283185307179586 * 5300.0 * t);
+        const double p1 = voss_pink(seed, i), p2 = voss_pink(seed ^ 0x5bd1e995ull, i);
+        double v[2] = {0.1 * p1 + tones, 0.07 * p1 + 0.03 * p2 + 0.8 * tones};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            double x = __builtin_rint(v[c] * 32767.0);
+            x = x > 32767.0 ? 32767.0 : (x < -32768.0 ? -32768.0 : x);
+            pcm[2 * i + c] = (int16_t)x;
+        }
     }
 }

@@ -1,19 +1,23 @@
 // pac_master.hip -- gfx950 kernels of the master (.wak) profile: codec/ of the
 // reference (M/S decision, six masking thresholds, bit reservoir, Huffman).
 //
-// Per chunk of Bc stereo blocks (whole-stream block ranges, stream-major):
+// Streams are processed in groups; a group is swept in time slices (chunk =
+// blocks t0..t0+S-1 of every stream of the group, PacMasterChunk), so the
+// serial reservoir chain of every stream of the group advances in parallel:
 //   k_master_thr    one wave per (block, variant): the six calcBTHR() calls of
 //                   getStereoMaskThreshold (psychoac.py:540-562) incl. the
 //                   in-place Hann chains -> thr[gb][v][1024]
 //   k_master_front  one wave per block: LRMS decision (codec.py:94-102), MDCT
 //                   L/R + overall scale (codec.py:237-246), M/S lines, MLD
 //                   combination and per-band SMR selection (psychoac.py:533-682)
-//   k_master_tail   one wave per STREAM, blocks in order: withdrawBits, the two
+//   k_master_tail   one wave per STREAM of the chunk, its blocks in order: withdrawBits, the two
 //                   BitAlloc calls with the extraBits carry (codec.py:222-260,
 //                   bitalloc.py:129-184), scale factors, 10-table Huffman
 //                   length scoring and depositBits (codec.py:111-124)
 //   k_master_pack   one wave per channel-block: sign bits, Huffman codes and
-//                   LRMS packed MSB-first (pacfile.py:288-351)
+//                   LRMS packed MSB-first (pacfile.py:288-351) into the
+//                   group's staging area at the stream's running cursor
+//   k_copy_streams  after a group: each stream's bytes to its final offset
 
 struct PacMasterWork {
     double* thr;        // [Bc][6][1024]
@@ -27,6 +31,25 @@ struct PacMasterWork {
     uint8_t* tid;       // [Bc][2]
     int32_t* nbytes;    // [Bc*2]
 };
+
+// A time slice of a stream group: blocks t0 .. t0+S-1 of streams
+// s_first .. s_first+n_s-1; local block j = (s - s_first) * S + (t - t0).
+struct PacMasterChunk {
+    int s_first, n_s;
+    int64_t t0;
+    int S;
+};
+
+// global block id of local block j, false if that stream has ended
+__device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off, const PacMasterChunk& ck,
+                                            int64_t j, int64_t* gb) {
+    const int s = ck.s_first + (int)(j / ck.S);
+    const int64_t t = ck.t0 + j % ck.S;
+    const int64_t b0 = blk_off[s];
+    if (t >= blk_off[s + 1] - b0) return false;
+    *gb = b0 + t;
+    return true;
+}
 
 // LRMS-variant signals: the in-place window chains of EncodeDualChannel and
 // getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
@@ -45,7 +68,7 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 }
 
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                         PacMasterWork W, int64_t gb0) {
+                                                         PacMasterWork W, PacMasterChunk ck) {
     __shared__ double2 buf[1024];
     __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // FFT / peak scratch, then beta rows
     const int tid = threadIdx.x;
@@ -54,15 +77,25 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
     const int64_t j = item / 6;                // block within the chunk
     const int v = (int)(item % 6);
-    const BlockPcm rL(locate(src, gb0 + j, 0));
-    const BlockPcm rR(locate(src, gb0 + j, 1));
+    int64_t gb;
+    if (!chunk_block(src.blk_off, ck, j, &gb)) return;     // uniform per workgroup
+    const BlockPcm rL(locate(src, gb, 0));
+    const BlockPcm rR(locate(src, gb, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta));
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
+    // rows claimed dynamically, most expensive first (as in k_origin_front)
+    int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));
+    if (tid == 0) *rowctr = 0;
+    __syncthreads();
 #pragma unroll 1
-    for (int i = 0; i < 4; ++i) {
-        int r = w + 4 * i;
+    while (true) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(rowctr, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k >= 16) break;
+        const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
         out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r, beta + w * 512);
     }
 }
@@ -134,14 +167,16 @@ __device__ __forceinline__ void wave_spectrum_cplx(const DS& d, const PacTables*
 }
 
 __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTables* __restrict__ T,
-                                                     PacMasterWork W, int64_t gb0) {
+                                                     PacMasterWork W, PacMasterChunk ck) {
     __shared__ double2 bufL[1024];      // 16 KB
     __shared__ double2 bufR[1024];      // 16 KB
     __shared__ uint8_t lrms_s[PAC_NB];
     const int lane = threadIdx.x;
     const int64_t j = blockIdx.x;
-    const BlockPcm rL(locate(src, gb0 + j, 0));
-    const BlockPcm rR(locate(src, gb0 + j, 1));
+    int64_t gb;
+    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    const BlockPcm rL(locate(src, gb, 0));
+    const BlockPcm rR(locate(src, gb, 1));
 
     // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:96-102)
     wave_spectrum_cplx([&](int i) { return rL(i); }, T, bufL, lane);
@@ -242,77 +277,68 @@ __global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTab
     }
 }
 
-// --- master BitAlloc (bitalloc.py:129-184), evaluated identically by every lane
+// --- master BitAlloc (bitalloc.py:129-184), band b on lane b ---------------
+// Each round gives one bit to the first band with the largest smr - 6 bits
+// among the still-valid bands (wave max + ballot: the serial loop's
+// first-index tie break); the stop test uses the max of smr - 6 (bits - 1)
+// over all bands, as the reference does.  Returns the bits left minus extra;
+// *ba_lane = this lane's band allocation.
 __device__ long bitalloc_master(const double* __restrict__ smr_g, const uint8_t* lrms,
                                 const PacTables* __restrict__ T, double bitBudget, long extra,
-                                int maxMantBits, int bits_out[PAC_NB]) {
-    double smr[PAC_NB];
-    int bits[PAC_NB], nl[PAC_NB], lr[PAC_NB];
-#pragma unroll
-    for (int b = 0; b < PAC_NB; ++b) {
-        smr[b] = smr_g[b];
-        bits[b] = 0;
-        nl[b] = T->nlines[b];
-        lr[b] = lrms[b];
-    }
-    unsigned valid = (1u << PAC_NB) - 1u;
+                                int maxMantBits, int lane, int* ba_lane) {
+    const bool band = lane < PAC_NB;
+    const double smr = band ? smr_g[lane] : 0.0;
+    const int nl = band ? T->nlines[lane] : 0;
+    const int lr = band ? lrms[lane] : 0;
+    int bits = 0;
+    bool valid = band;
     long total = (long)(bitBudget + (double)extra);
-    while (valid) {
-        int im = -1;
-        double best = 0.0;
-        double g = smr[0] - (bits[0] - 1) * 6.;
-#pragma unroll
-        for (int b = 0; b < PAC_NB; ++b) {
-            double v = smr[b] - bits[b] * 6.;
-            if (((valid >> b) & 1u) && (im < 0 || v > best)) { best = v; im = b; }
-            double w = smr[b] - (bits[b] - 1) * 6.;
-            g = w > g ? w : g;
-        }
-        int nli = 0, lri = 0, bi = 0;
-#pragma unroll
-        for (int b = 0; b < PAC_NB; ++b)
-            if (b == im) { nli = nl[b]; lri = lr[b]; bi = bits[b]; }
-        const unsigned bit = 1u << im;
-        if (g < (lri ? -5.0 : -15.0)) valid &= ~bit;
+    while (__ballot(valid)) {
+        const double v = smr - bits * 6.;
+        const double best = wave_ext_f64<true>(valid ? v : -INFINITY);
+        const unsigned long long win = __ballot(valid && v == best);
+        const int im = __builtin_ctzll(win);
+        const double g = wave_ext_f64<true>(band ? smr - (bits - 1) * 6. : -INFINITY);
+        const int nli = __builtin_amdgcn_readlane(nl, im);
+        const int lri = __builtin_amdgcn_readlane(lr, im);
+        const int bi = __builtin_amdgcn_readlane(bits, im);
+        bool drop = g < (lri ? -5.0 : -15.0);
         if (total - nli >= 0) {
-#pragma unroll
-            for (int b = 0; b < PAC_NB; ++b)
-                if (b == im) bits[b] += 1;
+            if (lane == im) bits += 1;
             total -= nli;
-            if (bi + 1 >= maxMantBits) valid &= ~bit;
+            drop |= bi + 1 >= maxMantBits;
         } else {
-            valid &= ~bit;
+            drop = true;
         }
+        if (lane == im && drop) valid = false;
     }
-#pragma unroll
-    for (int b = 0; b < PAC_NB; ++b) {
-        if (bits[b] == 1) { total += nl[b]; bits[b] = 0; }
-        bits_out[b] = bits[b];
-    }
+    int back = 0;
+    if (bits == 1) { back = nl; bits = 0; }
+    total += wave_sum_i(back);
+    *ba_lane = bits;
     return total - extra;
 }
 
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
-}
-
-// One wave per stream: the serial reservoir chain over the stream's blocks.
+// One wave per stream of the chunk: the serial reservoir chain over the
+// stream's blocks t0 .. t0+S-1, and the stream's running byte cursor (each
+// channel-block's staging offset, in file order).
 __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict__ T,
                                                     const PacHuffTables* __restrict__ H,
                                                     PacMasterWork W, const int64_t* __restrict__ blk_off,
-                                                    int s0, int64_t gb0, int64_t gb1,
-                                                    int64_t* __restrict__ st_extra,
-                                                    int64_t* __restrict__ st_deposit, double bitBudget) {
+                                                    PacMasterChunk ck, int64_t* __restrict__ st_extra,
+                                                    int64_t* __restrict__ st_deposit,
+                                                    int64_t* __restrict__ st_cursor,
+                                                    int64_t* __restrict__ off, double bitBudget) {
     __shared__ int ba_s[PAC_NB], sf_s[PAC_NB];
     const int lane = threadIdx.x;
-    const int s = s0 + blockIdx.x;
-    int64_t b_begin = blk_off[s] > gb0 ? blk_off[s] : gb0;
-    int64_t b_end = blk_off[s + 1] < gb1 ? blk_off[s + 1] : gb1;
+    const int sl = blockIdx.x;
+    const int s = ck.s_first + sl;
+    const int64_t len = blk_off[s + 1] - blk_off[s];
+    const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
     long extra = st_extra[s], deposit = st_deposit[s];
-    for (int64_t gb = b_begin; gb < b_end; ++gb) {
-        const int64_t j = gb - gb0;
+    int64_t cur = st_cursor[s];
+    for (int64_t t = ck.t0; t < t_end; ++t) {
+        const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
         // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
         long e = 0;
         if (deposit > 10) { e = deposit / 100; deposit -= e; }
@@ -320,62 +346,62 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
         extra += e;
         long dep_add = 0;
         for (int ch = 0; ch < 2; ++ch) {
-            int bits[PAC_NB];
-            long diff = bitalloc_master(W.smr + (j * 2 + ch) * PAC_NB, W.lrms + j * PAC_NB, T,
-                                        bitBudget, extra, 16, bits);
+            const int64_t g = j * 2 + ch;
+            int ba;
+            const long diff = bitalloc_master(W.smr + g * PAC_NB, W.lrms + j * PAC_NB, T, bitBudget, extra, 16,
+                                              lane, &ba);
             extra += diff;
             if (lane < PAC_NB) {
-                int ba = 0;
-#pragma unroll
-                for (int b = 0; b < PAC_NB; ++b)
-                    if (b == lane) ba = bits[b];
                 ba_s[lane] = ba;
-                int sf = pac_scale_factor(W.bandpeak[(j * 2 + ch) * PAC_NB + lane], ba);
+                const int sf = pac_scale_factor(W.bandpeak[g * PAC_NB + lane], ba);
                 sf_s[lane] = sf;
-                W.ba[(j * 2 + ch) * PAC_NB + lane] = (uint8_t)ba;
-                W.sf[(j * 2 + ch) * PAC_NB + lane] = (uint8_t)sf;
+                W.ba[g * PAC_NB + lane] = (uint8_t)ba;
+                W.sf[g * PAC_NB + lane] = (uint8_t)sf;
             }
             wave_sync();
             // StripSignBits + Huffman.encodeData scoring of the 10 tables
-            const double* ln = W.lines + (j * 2 + ch) * PAC_HALFN;
+            const double* ln = W.lines + g * PAC_HALFN;
             int acc[PAC_NTAB];
 #pragma unroll
-            for (int t = 0; t < PAC_NTAB; ++t) acc[t] = 0;
+            for (int tb = 0; tb < PAC_NTAB; ++tb) acc[tb] = 0;
             int nsign = 0, orig = 0;
             for (int q = 0; q < 16; ++q) {
-                int l = q * WAVE + lane;
-                int b = T->band_of_line[l];
-                int ba = ba_s[b];
-                if (!ba) continue;
-                uint32_t m = pac_mantissa(ln[l], sf_s[b], ba);
-                uint32_t sym = m & ((1u << (ba - 1)) - 1u);
+                const int l = q * WAVE + lane;
+                const int b = T->band_of_line[l];
+                const int bal = ba_s[b];
+                if (!bal) continue;
+                const uint32_t m = pac_mantissa(ln[l], sf_s[b], bal);
+                const uint32_t sym = m & ((1u << (bal - 1)) - 1u);
                 nsign += 1;
-                orig += ba;
+                orig += bal;
 #pragma unroll
-                for (int t = 0; t < PAC_NTAB; ++t) {
-                    int L = H->len[t][sym];
-                    acc[t] += L ? L : H->esc_len[t] + ba;
+                for (int tb = 0; tb < PAC_NTAB; ++tb) {
+                    const int L = H->len[tb][sym];
+                    acc[tb] += L ? L : H->esc_len[tb] + bal;
                 }
             }
             nsign = wave_sum_i(nsign);
             orig = wave_sum_i(orig);
             int best = 0, bestid = 1;
 #pragma unroll
-            for (int t = 0; t < PAC_NTAB; ++t) {
-                int v = wave_sum_i(acc[t]);
-                if (t == 0 || v < best) { best = v; bestid = t + 1; }
+            for (int tb = 0; tb < PAC_NTAB; ++tb) {
+                const int v = wave_sum_i(acc[tb]);
+                if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
             }
             dep_add += (long)orig - ((long)best + nsign + 4);
-            int nbits = 8 + 8 * PAC_NB + nsign + best + PAC_NB;
+            const int nbits = 8 + 8 * PAC_NB + nsign + best + PAC_NB;
+            const int nbytes = 4 + (nbits + 7) / 8;
             if (lane == 0) {
-                W.tid[j * 2 + ch] = (uint8_t)bestid;
-                W.nbytes[j * 2 + ch] = 4 + (nbits + 7) / 8;
+                W.tid[g] = (uint8_t)bestid;
+                W.nbytes[g] = nbytes;
+                off[g] = cur;
             }
+            cur += nbytes;
             wave_sync();
         }
         deposit += dep_add;     // depositBits per channel (codec.py:120)
     }
-    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
+    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; st_cursor[s] = cur; }
 }
 
 __device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
@@ -392,16 +418,17 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
 // One wave per channel-block g = 2*j + ch of the chunk.
 __global__ __launch_bounds__(64) void k_master_pack(const PacTables* __restrict__ T,
                                                     const PacHuffTables* __restrict__ H,
-                                                    PacMasterWork W, const int64_t* __restrict__ off,
-                                                    const int64_t* __restrict__ base,
-                                                    uint8_t* __restrict__ out) {
+                                                    PacMasterWork W, const int64_t* __restrict__ blk_off,
+                                                    PacMasterChunk ck, const int64_t* __restrict__ off,
+                                                    uint8_t* __restrict__ stage) {
     __shared__ uint32_t words[PACK_WORDS];
     __shared__ int bas[PAC_NB], sfs[PAC_NB], bstart[PAC_NB + 1];
     __shared__ int rowsum[16];
     const int lane = threadIdx.x;
     const int64_t g = blockIdx.x;
     const int64_t j = g >> 1;
-    const int ch = (int)(g & 1);
+    int64_t gb;
+    if (!chunk_block(blk_off, ck, j, &gb)) return;
     for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
     if (lane < PAC_NB) {
         bas[lane] = W.ba[g * PAC_NB + lane];
@@ -486,19 +513,19 @@ __global__ __launch_bounds__(64) void k_master_pack(const PacTables* __restrict_
     }
     wave_sync();
     const int nbytes = W.nbytes[g] - 4;
-    store_block_bytes(out + *base + off[g], words, nbytes, lane);
+    store_block_bytes(stage + off[g], words, nbytes, lane);
 }
 
-__global__ void k_add_base(int64_t* __restrict__ base, const int64_t* __restrict__ total) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *base += *total;
-}
-
-// stream start offsets for streams whose first block lies in [gb0, gb1)
-__global__ void k_master_stream_offsets(const int64_t* __restrict__ off, const int64_t* __restrict__ blk_off,
-                                        int n_streams, int64_t gb0, int64_t gb1,
-                                        const int64_t* __restrict__ base, int64_t* __restrict__ so) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_streams) return;
-    int64_t b = blk_off[s];
-    if (b >= gb0 && b < gb1) so[s] = *base + off[(b - gb0) * 2];
+// after a stream group: every stream's bytes from its staging area to its
+// final offset (one workgroup per stream)
+__global__ __launch_bounds__(256) void k_copy_streams(const uint8_t* __restrict__ stage,
+                                                      const int64_t* __restrict__ src_off,
+                                                      const int64_t* __restrict__ dst_off,
+                                                      const int64_t* __restrict__ size,
+                                                      uint8_t* __restrict__ out) {
+    const int s = blockIdx.x;
+    const uint8_t* a = stage + src_off[s];
+    uint8_t* b = out + dst_off[s];
+    const int64_t n = size[s];
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) b[i] = a[i];
 }

@@ -59,6 +59,15 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     v += dpp_f64<PAC_DPP_BCAST31, 0xc>(0.0, v);        // rows 2, 3 += rows 0 + 1
     return readlane_f64(v, 63);
 }
+__device__ __forceinline__ int wave_sum_i(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_QXOR1, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_QXOR2, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_HMIRROR, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_MIRROR, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_BCAST15, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, PAC_DPP_BCAST31, 0xc, 0xf, false);
+    return __builtin_amdgcn_readlane(v, 63);
+}
 template <bool MAX>
 __device__ __forceinline__ double wave_ext_f64(double v) {
     auto f = [](double a, double b) { return MAX ? fmax(a, b) : fmin(a, b); };
@@ -260,6 +269,10 @@ __device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* 
 #define PAC_LOG2_10_OVER_10 0.33219280948873624   // log2(10)/10
 #define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
 #define PAC_LN2 0.6931471805599453
+// order in which the 16 masking rows (64 lines each) are claimed by the waves
+// of a threshold kernel, 4 bits per row, most expensive first (measured on
+// broadband input: the middle rows carry the most maskers on both sides)
+#define PAC_ROW_ORDER 0xf0e1dc4528b9a763ull
 #define PAC_MOM_MIN 24      // fewest common upper maskers for the moment form
 #define PAC_MOM_DMAX 40     // highest Taylor degree of the moment form
 

@@ -144,21 +144,50 @@ def cpu_baseline(ctx, dev_pcm, frames_per_stream, n_streams, fs, seconds, profil
 
     def work(t):
         o = P.Oracle(fs, huffman=(prof == P.MASTER))
-        done, chunk = 0, 16
+        done, chunk, last = 0, 16, b""
         while time.perf_counter() - t0 < seconds and done < 200000:
             n = min(chunk, hops - 1)
-            o.encode_data(prof, pcms[t][: n * 1024], max_blocks=n)
+            last = o.encode_data(prof, pcms[t][: n * 1024], max_blocks=n)
             done += n
             chunk = min(chunk * 2, hops - 1)
-        return done
+        return done, last
 
     with ThreadPoolExecutor(threads) as ex:
-        done = sum(ex.map(work, range(threads)))
+        res = list(ex.map(work, range(threads)))
     el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
+    done = sum(r[0] for r in res)
+    base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
                       "fixtures), %s profile, %d host threads (one stream each), %d stereo "
                       "blocks of the same synthetic streams in %.1f s" % (profile, threads, done, el)}
+    return base, [r[1] for r in res]
+
+
+def channel_blocks(b):
+    """split a data section into its '<L nBytes' + payload channel-blocks"""
+    out, pos = [], 0
+    while pos + 4 <= len(b):
+        n = int.from_bytes(b[pos:pos + 4], "little")
+        out.append(b[pos:pos + 4 + n])
+        pos += 4 + n
+    return out
+
+
+def parity_check(ctx, out_dev, so, oracle_prefixes):
+    """The oracle's bytes for the first blocks of streams 0..T-1 (from the CPU
+    baseline run) against the GPU's bytes for the same streams: the number of
+    channel-blocks compared and how many differ (flip rate)."""
+    checked = bad = 0
+    for t, ref in enumerate(oracle_prefixes):
+        if not ref:
+            continue
+        got = np.empty(len(ref), dtype=np.uint8)
+        ctx.to_host(got, out_dev + int(so[t]))
+        a, b = channel_blocks(ref), channel_blocks(got.tobytes())
+        checked += len(a)
+        bad += sum(1 for x, y in zip(a, b) if x != y) + max(0, len(a) - len(b))
+    return {"checked_channel_blocks": checked, "mismatching": bad,
+            "against": "oracle/pac_oracle.c on the CPU-baseline sample"}
 
 
 def main():
@@ -270,8 +299,9 @@ def main():
         "out_bytes_per_gpu": out_bytes,
     }
     if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(ctx, pcm_dev, fps, ns, fs, a.cpu_seconds, a.profile,
-                                           a.cpu_threads)
+        res["cpu_baseline"], prefixes = cpu_baseline(ctx, pcm_dev, fps, ns, fs, a.cpu_seconds, a.profile,
+                                                     a.cpu_threads)
+        res["parity"] = parity_check(ctx, out_dev, so, prefixes)
     ctx.free(out_dev)
     ctx.free(pcm_dev)
     if dist.rank == 0:

@@ -64,6 +64,12 @@ struct pac_oracle {
     uint32_t esc_bits[PAC_NTABLES];
     uint8_t *hlen;                  /* [PAC_NTABLES][32768], 0 = absent */
     uint32_t *hbits;                /* [PAC_NTABLES][32768] */
+    /* decoder: Huffman code trees (node pairs; >0 child node, <0 leaf -(sym+2),
+     * -1 the escape code) built from the same tables, Huffman.py:321-344 */
+    int32_t *htree[PAC_NTABLES];
+    /* IMDCT twiddles, mdct.py:75,79 */
+    double ipre_c[N], ipre_s[N];    /* exp(j 2 pi k n0 / N) */
+    double ipost_c[N], ipost_s[N];  /* exp(j 2 pi (n + n0) / 2N) */
 };
 
 static double Bark(double f) {       /* psychoac.py:56-64 */
@@ -151,6 +157,17 @@ pac_oracle *pac_oracle_create(int fs) {
         t->fft_c[k] = cos(a);
         t->fft_s[k] = sin(a);
     }
+    for (int k = 0; k < N; k++) {
+        /* mdct.py:75: 1j*2.*pi*k*n0/N, numpy evaluation order */
+        double a = ((2.0 * M_PI) * (double)k) * 512.5;
+        a = a / (double)N;
+        t->ipre_c[k] = cos(a);
+        t->ipre_s[k] = sin(a);
+        /* mdct.py:79: 1j*2*pi/(2.*N)*(n+n0) */
+        double b = ((2.0 * M_PI) / (2.0 * N)) * ((double)k + 512.5);
+        t->ipost_c[k] = cos(b);
+        t->ipost_s[k] = sin(b);
+    }
     int step = fs / N;   /* Py2 integer division (sampleRate/N), psychoac.py:188 */
     for (int k = 0; k < HALFN; k++) {
         /* psychoac.py:434: sampleRate / 2.0 / nMDCTLines * (arange + 0.5) */
@@ -176,6 +193,7 @@ pac_oracle *pac_oracle_create(int fs) {
 
 void pac_oracle_destroy(pac_oracle *t) {
     if (!t) return;
+    for (int i = 0; i < PAC_NTABLES; i++) free(t->htree[i]);
     free(t->hlen);
     free(t->hbits);
     free(t);
@@ -219,6 +237,29 @@ int pac_oracle_load_huffman(pac_oracle *t, const uint8_t *buf, int64_t len) {
         }
     }
     t->have_huff = 1;
+    /* decoding trees: insert every code (and the escape code) bit by bit */
+    for (int id = 0; id < PAC_NTABLES; id++) {
+        int64_t cap = 2;
+        for (int sym = 0; sym < PAC_NSYM; sym++) cap += 2 * (int64_t)t->hlen[id * PAC_NSYM + sym];
+        cap += 2 * (int64_t)t->esc_len[id] + 2;
+        int32_t *tr = (int32_t *)calloc((size_t)cap, sizeof(int32_t));
+        if (!tr) return -8;
+        int32_t next = 1;            /* node 0 = root, node i occupies tr[2i], tr[2i+1] */
+        for (int sym = -1; sym < PAC_NSYM; sym++) {
+            int len = sym < 0 ? t->esc_len[id] : t->hlen[id * PAC_NSYM + sym];
+            uint32_t code = sym < 0 ? t->esc_bits[id] : t->hbits[id * PAC_NSYM + sym];
+            if (!len) continue;
+            int32_t node = 0;
+            for (int i = len - 1; i >= 0; i--) {
+                int bit = (code >> i) & 1u;
+                int32_t *slot = &tr[2 * node + bit];
+                if (i == 0) { *slot = sym < 0 ? -1 : -(sym + 2); break; }
+                if (*slot <= 0) *slot = next++;
+                node = *slot;
+            }
+        }
+        t->htree[id] = tr;
+    }
     return 0;
 }
 
@@ -719,6 +760,183 @@ static int64_t emit_master(const pac_oracle *t, const pac_oracle_stblock *o, int
     }
     for (int b = 0; b < NB; b++) put(&w, (uint32_t)o->lrms[b], 1);
     return k + nbytes;
+}
+
+/* ------------------------------------------------------------------------ */
+/* decoder: PACFile.ReadDataBlock (pacfile.py:153-229; Origin pacfile.py    */
+/* ReadDataBlock), codec.Decode (codec.py:25-65; Origin codec.py Decode),   */
+/* the decode driver (pacfile.py:478-499) and PCMFile.WriteDataBlock        */
+/* (pcmfile.py:118-147)                                                     */
+/* ------------------------------------------------------------------------ */
+
+typedef struct { const uint8_t *p; int64_t n, bit; } br;
+static uint32_t get(br *r, int nb) {                    /* PackedBits.ReadBits, MSB-first */
+    uint32_t v = 0;
+    for (int i = 0; i < nb; i++, r->bit++) {
+        int b = (r->bit >> 3) < r->n ? (r->p[r->bit >> 3] >> (7 - (r->bit & 7))) & 1 : 0;
+        v = (v << 1) | (uint32_t)b;
+    }
+    return v;
+}
+
+/* Huffman.decodeData (Huffman.py:321-344): walk the code tree bit by bit;
+ * the escape code is followed by the raw ba-bit symbol */
+static uint32_t huff_decode(const pac_oracle *t, br *r, int id, int ba) {
+    const int32_t *tr = t->htree[id];
+    int32_t node = 0;
+    for (;;) {
+        int32_t v = tr[2 * node + (int)get(r, 1)];
+        if (v == -1) return get(r, ba);
+        if (v < -1) return (uint32_t)(-v - 2);
+        if (v == 0) return 0;                 /* not a code of the table: malformed input */
+        node = v;
+    }
+}
+
+/* vDequantize (quantize.py:345-376) + vDequantizeUniform (:118-145), nScaleBits 4 */
+static double dequantize(int scale, int64_t m, int ba) {
+    const int64_t smask = (int64_t)1 << (ba - 1);
+    const int neg = (m & smask) == smask;
+    if (neg) m -= smask;
+    int64_t q = m << (15 - scale);
+    if (scale < 15 && m > 0) q += (int64_t)1 << (15 - scale - 1);
+    const int R = ba + 15;
+    const int64_t sm = (int64_t)1 << (R - 1);
+    if (neg) q += sm;
+    const double largest = (double)(sm << 1) - 1.0;
+    const int neg2 = (q & sm) == sm;
+    if (neg2) q -= sm;
+    const double a = 2.0 * (double)q / largest;
+    return neg2 ? -a : a;
+}
+
+/* IMDCT mdct.py:72-79 (a=b=1024, numpy formula) followed by SineWindow */
+void pac_oracle_imdct_window(const pac_oracle *t, const double *X, double *y) {
+    double re[N], im[N];
+    for (int k = 0; k < N; k++) {
+        const double v = k < HALFN ? X[k] : -X[N - 1 - k];     /* hstack((data, -data[::-1])) */
+        re[k] = v * t->ipre_c[k];
+        im[k] = -(v * t->ipre_s[k]);                          /* conj: ifft via the forward FFT */
+    }
+    fft2048(t, re, im);
+    for (int n = 0; n < N; n++) {
+        const double ar = re[n] / (double)N, ai = -im[n] / (double)N;   /* numpy ifft: 1/N */
+        const double post = (double)N * (ar * t->ipost_c[n] - ai * t->ipost_s[n]);
+        y[n] = post * t->sine[n];
+    }
+}
+
+/* PCMFile.WriteDataBlock sample conversion: sign, vQuantizeUniform(|x|, 16), re-sign */
+int16_t pac_oracle_float_to_pcm(double x) {
+    const int s = signbit(x) != 0;
+    const double a = s ? -x : x;
+    const uint64_t code = a < 1.0 ? (uint64_t)((a * 65535.0 + 1.0) / 2.0) : 32767u;
+    const int16_t c = (int16_t)code;
+    return s ? (int16_t)-c : c;
+}
+
+/* one channel-block's fields from its nBytes of data */
+static void parse_chblock(const pac_oracle *t, int profile, const uint8_t *p, int64_t n, int *overall,
+                          int *ba, int *sf, int64_t *mant, int *lrms) {
+    br r = {p, n, 0};
+    *overall = (int)get(&r, 4);
+    int id = profile == PAC_ORACLE_MASTER ? (int)get(&r, 4) - 1 : 0;
+    memset(mant, 0, sizeof(int64_t) * HALFN);
+    for (int b = 0; b < NB; b++) {
+        int a = (int)get(&r, 4);
+        if (a) a++;
+        ba[b] = a;
+        sf[b] = (int)get(&r, 4);
+        if (!a) continue;
+        if (profile == PAC_ORACLE_ORIGIN) {
+            for (int l = t->lower[b]; l <= t->upper[b]; l++) mant[l] = get(&r, a);
+        } else {
+            uint32_t sg[HALFN];
+            for (int l = t->lower[b]; l <= t->upper[b]; l++) sg[l] = get(&r, 1);
+            for (int l = t->lower[b]; l <= t->upper[b]; l++)
+                mant[l] = (int64_t)huff_decode(t, &r, id, a) + (int64_t)sg[l] * ((int64_t)1 << (a - 1));
+        }
+    }
+    if (profile == PAC_ORACLE_MASTER)
+        for (int b = 0; b < NB; b++) lrms[b] = (int)get(&r, 1);
+}
+
+/* Decode the data section of a .pac/.wak file (everything after the header)
+ * exactly as the reference's decode driver writes the output WAV: blocks of
+ * 1024 frames, the first ReadDataBlock result skipped, the final overlap half
+ * written.  pcm: int16 interleaved; fout (optional): the same samples as
+ * float64 before conversion.  Returns the frames written or < 0. */
+int64_t pac_oracle_decode(const pac_oracle *t, int profile, const uint8_t *data, int64_t nbytes, int n_ch,
+                          int16_t *pcm, double *fout, int64_t max_frames) {
+    if (n_ch < 1 || n_ch > 8) return -1;
+    if (profile == PAC_ORACLE_MASTER && (n_ch != 2 || !t->have_huff)) return -1;
+    double *prev = (double *)calloc((size_t)n_ch * HALFN, sizeof(double));
+    double *lines = (double *)malloc((size_t)n_ch * HALFN * sizeof(double));
+    double *y = (double *)malloc((size_t)n_ch * N * sizeof(double));
+    int64_t *mant = (int64_t *)malloc((size_t)n_ch * HALFN * sizeof(int64_t));
+    int64_t pos = 0, frames = 0;
+    int first = 1, ret = 0;
+    for (;;) {
+        int eof = pos + 4 > nbytes;
+        int lrms[NB] = {0};
+        if (!eof) {
+            for (int c = 0; c < n_ch; c++) {
+                if (pos + 4 > nbytes) { ret = -3; goto done; }
+                uint32_t nb = (uint32_t)data[pos] | ((uint32_t)data[pos + 1] << 8) |
+                              ((uint32_t)data[pos + 2] << 16) | ((uint32_t)data[pos + 3] << 24);
+                pos += 4;
+                if (pos + (int64_t)nb > nbytes) { ret = -3; goto done; }
+                int overall, ba[NB], sf[NB];
+                parse_chblock(t, profile, data + pos, nb, &overall, ba, sf, mant + c * HALFN, lrms);
+                pos += nb;
+                /* codec.Decode: dequantize the bands with bits, then / 2^overall */
+                double *L = lines + c * HALFN;
+                memset(L, 0, sizeof(double) * HALFN);
+                for (int b = 0; b < NB; b++)
+                    if (ba[b])
+                        for (int l = t->lower[b]; l <= t->upper[b]; l++)
+                            L[l] = dequantize(sf[b], mant[c * HALFN + l], ba[b]);
+                const double rescale = 1. * (double)(1 << overall);
+                for (int l = 0; l < HALFN; l++) L[l] /= rescale;
+            }
+            if (profile == PAC_ORACLE_MASTER) {
+                /* codec.py:46-54.  mdctLineL/R ALIAS mdctLine[0]/[1], so the
+                 * second assignment reads the already-updated channel 0:
+                 * L = M - S, R = (M - S) + S */
+                double *A = lines, *B = lines + HALFN;
+                for (int b = 0; b < NB; b++) {
+                    if (!lrms[b]) continue;
+                    for (int l = t->lower[b]; l <= t->upper[b]; l++) {
+                        A[l] = A[l] - B[l];
+                        B[l] = A[l] + B[l];
+                    }
+                }
+            }
+            for (int c = 0; c < n_ch; c++) pac_oracle_imdct_window(t, lines + c * HALFN, y + c * N);
+        }
+        if (!eof || 1) {
+            /* ReadDataBlock's result: overlap-add of the first half (or, at
+             * the end of the file, the saved half alone) */
+            if (!first) {
+                if (frames + HALFN > max_frames) { ret = -2; goto done; }
+                for (int i = 0; i < HALFN; i++)
+                    for (int c = 0; c < n_ch; c++) {
+                        double v = eof ? prev[c * HALFN + i] : prev[c * HALFN + i] + y[c * N + i];
+                        int64_t o = (frames + i) * n_ch + c;
+                        pcm[o] = pac_oracle_float_to_pcm(v);
+                        if (fout) fout[o] = v;
+                    }
+                frames += HALFN;
+            }
+            first = 0;
+        }
+        if (eof) break;
+        for (int c = 0; c < n_ch; c++) memcpy(prev + c * HALFN, y + c * N + HALFN, sizeof(double) * HALFN);
+    }
+    ret = 0;
+done:
+    free(prev); free(lines); free(y); free(mant);
+    return ret < 0 ? ret : frames;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -62,6 +62,10 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
 int64_t pac_oracle_encode(const pac_oracle *t, int profile, const int16_t *pcm,
                           int64_t n_frames, int n_ch, int64_t max_blocks,
                           uint8_t *out, int64_t cap, pac_oracle_state *state);
+void pac_oracle_imdct_window(const pac_oracle *t, const double *X, double *y);
+int16_t pac_oracle_float_to_pcm(double x);
+int64_t pac_oracle_decode(const pac_oracle *t, int profile, const uint8_t *data, int64_t nbytes, int n_ch,
+                          int16_t *pcm, double *fout, int64_t max_frames);
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,12 @@ def lib():
         L.pac_oracle_block_origin.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(ChBlock)]
         L.pac_oracle_block_master.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
                                               C.POINTER(State), C.POINTER(StBlock)]
+        L.pac_oracle_decode.restype = C.c_int64
+        L.pac_oracle_decode.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int64, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_int64]
+        L.pac_oracle_imdct_window.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.pac_oracle_float_to_pcm.restype = C.c_int16
+        L.pac_oracle_float_to_pcm.argtypes = [C.c_double]
         L.pac_oracle_encode.restype = C.c_int64
         L.pac_oracle_encode.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int,
                                         C.c_int64, C.c_void_p, C.c_int64, C.POINTER(State)]
@@ -137,6 +143,61 @@ class Oracle:
         if n < 0:
             raise RuntimeError("oracle encode failed %d" % n)
         return out[:n].tobytes()
+
+
+def _decode_method(self, profile, data, n_ch, want_float=False):
+    """Decode a data section (bytes after the PAC header) like the
+    reference's decode driver: int16 frames [n, n_ch] (+ float64 samples)."""
+    nblocks = max(len(data) // 4, 1)
+    cap = (nblocks + 1) * 1024
+    pcm = np.zeros((cap, n_ch), dtype=np.int16)
+    fo = np.zeros((cap, n_ch)) if want_float else None
+    n = self.L.pac_oracle_decode(self.h, profile, bytes(data), len(data), n_ch, pcm.ctypes.data,
+                                 fo.ctypes.data if want_float else None, cap)
+    if n < 0:
+        raise RuntimeError("oracle decode failed %d" % n)
+    return (pcm[:n], fo[:n]) if want_float else pcm[:n]
+
+
+def _imdct_method(self, X):
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.zeros(2048)
+    self.L.pac_oracle_imdct_window(self.h, X.ctypes.data, y.ctypes.data)
+    return y
+
+
+Oracle.decode_data = _decode_method
+Oracle.imdct_window = _imdct_method
+
+
+def parse_pac_header(b):
+    """PACFile.ReadFileHeader (pacfile.py:115-151): (fs, nch, numSamples,
+    nlines, data offset)"""
+    assert b[:4] == b"PAC "
+    fs, nch, ns, nmdct, nsb, nmb = struct.unpack("<LHLLHH", b[4:22])
+    nb = struct.unpack("<L", b[22:26])[0]
+    nl = struct.unpack("<%dH" % nb, b[26:26 + 2 * nb])
+    return fs, nch, ns, list(nl), 26 + 2 * nb
+
+
+def wav_bytes(fs, nch, num_samples, frames):
+    """PCMFile.WriteFileHeader (pcmfile.py:103-116; sizes from numSamples)
+    followed by the frames written block by block"""
+    data_bytes = num_samples * nch * 2
+    h = struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + data_bytes, b"WAVE", b"fmt ", 16, 1, nch, fs,
+                    fs * nch * 2, nch * 2, 16, b"data", data_bytes)
+    return h + np.ascontiguousarray(frames, dtype="<i2").tobytes()
+
+
+def decode_file(path, profile):
+    """the reference decode driver (pacfile.py:430-499) on a .pac/.wak file:
+    the output WAV file's bytes"""
+    with open(path, "rb") as f:
+        b = f.read()
+    fs, nch, ns, nl, off = parse_pac_header(b)
+    o = Oracle(fs, huffman=(profile == MASTER))
+    pcm = o.decode_data(profile, b[off:], nch)
+    return wav_bytes(fs, nch, ns, pcm)
 
 
 def read_wav(path):

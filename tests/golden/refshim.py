@@ -194,6 +194,29 @@ def encode(inp, out, profile):
     else: outFile.WriteDataBlock(z, cp, huffman)
     outFile.fp.close()
     return cp, huffman
+
+
+def decode(inp, out, profile):
+    """Mirror of the reference driver (pacfile.py __main__ decode half)."""
+    huffman = None
+    if profile == "master":
+        from Huffman import Huffman
+        huffman = Huffman()
+    inFile = PACFile(inp); outFile = PCMFile(out)
+    cp = inFile.OpenForReading()
+    cp.bitsPerSample = 16
+    if profile == "master": cp.nTableIDBits = 4
+    outFile.OpenForWriting(cp)
+    first = True
+    while True:
+        data = inFile.ReadDataBlock(cp, huffman) if huffman is not None else inFile.ReadDataBlock(cp)
+        if not data: break
+        if first:
+            first = False
+            continue
+        outFile.WriteDataBlock(data, cp)
+    inFile.Close(cp)
+    outFile.Close(cp)
 '''
 
 

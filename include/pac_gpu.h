@@ -120,6 +120,23 @@ int pac_encode_block(pac_ctx *ctx, const pac_params *p, const double *full_block
                      pac_stream_state *state, uint8_t *out, int64_t out_capacity,
                      int64_t *out_bytes, pac_block_fields *fields);
 
+/* Decode n independent .pac/.wak data sections (the bytes after each file's
+ * header, back to back, delimited by stream_byte_offsets[n+1] -- what
+ * pac_encode_streams writes) into 16-bit PCM, exactly as the reference's
+ * decode driver writes the output WAV's frames (pacfile.py:478-499):
+ * PACFile.ReadDataBlock (pacfile.py:153-229) + codec.Decode (codec.py:25-65)
+ * per block, the first ReadDataBlock result skipped, the final overlap half
+ * written, PCMFile.WriteDataBlock's conversion (pcmfile.py:118-147).  With
+ * preroll != 0 every ReadDataBlock result is kept (the PACFile plugin
+ * surface).  frame_offsets[n+1] (out) are filled first; if pcm_out is NULL
+ * or pcm_capacity_frames is too small the call returns PAC_E_CAPACITY after
+ * filling them.  float_out (optional, host): the same samples as float64
+ * before the int16 conversion.  pcm_out interleaved [frames][n_channels]. */
+int pac_decode_streams(pac_ctx *ctx, const pac_params *p, int32_t n_streams, const uint8_t *data,
+                       const int64_t *stream_byte_offsets, int32_t data_is_device, int32_t preroll,
+                       int16_t *pcm_out, int64_t pcm_capacity_frames, int32_t pcm_is_device,
+                       double *float_out, int64_t *frame_offsets);
+
 /* --- device buffers, sync, timing (benchmarks; data resident in HBM) ----- */
 int pac_device_alloc(pac_ctx *ctx, int64_t bytes, void **ptr);
 int pac_device_free(pac_ctx *ctx, void *ptr);

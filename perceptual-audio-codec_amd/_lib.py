@@ -76,6 +76,8 @@ def lib():
         "pac_encode_streams": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, vp,
                                          i64, i32, C.POINTER(i64), C.POINTER(StreamState)]),
         "pac_encode_bound": (i64, [C.POINTER(Params), i32, C.POINTER(i64)]),
+        "pac_decode_streams": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, i32, vp, i64,
+                                         i32, vp, C.POINTER(i64)]),
         "pac_encode_block": (C.c_int, [vp, C.POINTER(Params), vp, C.POINTER(StreamState), vp, i64,
                                        C.POINTER(i64), C.POINTER(BlockFields)]),
         "pac_device_alloc": (C.c_int, [vp, i64, C.POINTER(vp)]),
@@ -173,6 +175,45 @@ class Context:
             for i in range(ns):
                 states[i] = st[i]
         return out, so
+
+    def decode_streams(self, params, data, stream_offsets, preroll=False, want_float=False,
+                       data_is_device=False, out=None, out_capacity_frames=None, out_is_device=False):
+        """Decode data sections (bytes / uint8 array, or a device pointer when
+        data_is_device) delimited by stream_offsets.  Returns (pcm, frame
+        offsets, float samples or None); pcm is int16 [frames, nCh] unless
+        out_is_device (then `out` is returned)."""
+        so = np.ascontiguousarray(stream_offsets, dtype=np.int64)
+        ns = len(so) - 1
+        fo = np.zeros(ns + 1, dtype=np.int64)
+        if data_is_device:
+            dptr = data
+        else:
+            buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+            buf = np.ascontiguousarray(buf, dtype=np.uint8)
+            dptr = buf.ctypes.data
+        nch = params.n_channels
+        args = [self.h, C.byref(params), ns, dptr, so.ctypes.data_as(C.POINTER(C.c_int64)),
+                int(bool(data_is_device)), int(bool(preroll))]
+        fo_p = fo.ctypes.data_as(C.POINTER(C.c_int64))
+        if out is None:      # size query first (fills the frame offsets)
+            rc = self.L.pac_decode_streams(*args, None, 0, 0, None, fo_p)
+            if rc not in (PAC_OK, -6):
+                check(rc)
+            frames = int(fo[-1])
+            if out_is_device:
+                raise ValueError("out_is_device needs an out pointer")
+            out = np.zeros((max(frames, 1), nch), dtype=np.int16)
+            cap = frames
+        else:
+            cap = out_capacity_frames if out_capacity_frames is not None else out.shape[0]
+        fl = np.zeros((max(int(fo[-1]) if fo[-1] else cap, 1), nch)) if want_float else None
+        optr = out if out_is_device else out.ctypes.data
+        check(self.L.pac_decode_streams(*args, optr, int(cap), int(bool(out_is_device)),
+                                        fl.ctypes.data if want_float else None, fo_p))
+        frames = int(fo[-1])
+        if out_is_device:
+            return out, fo, (fl[:frames] if want_float else None)
+        return out[:frames], fo, (fl[:frames] if want_float else None)
 
     def encode_block(self, params, full_block, state=None):
         fb = np.ascontiguousarray(full_block, dtype=np.float64)

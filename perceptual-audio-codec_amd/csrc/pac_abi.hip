@@ -19,6 +19,7 @@
 #include "../../include/pac_gpu.h"
 #include "pac_kernels.hip"
 #include "pac_master.hip"
+#include "pac_decode.hip"
 
 #define PAC_VERSION 100
 
@@ -202,6 +203,14 @@ struct pac_ctx {
     int64_t stage_max = (int64_t)16 << 30;  // bytes of worst-case output per stream group
     PacHuffTables* huff_host = nullptr;
     std::unordered_map<uint64_t, int> huff_dec[PAC_NTAB];   // (len<<32|code) -> symbol, -1 = escape
+    // decoder
+    DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)
+    PacHuffDec hdec = {};
+    DevBuf<uint8_t> dec_data, dec_ba, dec_sf, dec_ov, dec_lrms;
+    DevBuf<uint16_t> dec_codes;
+    DevBuf<int64_t> dec_so, dec_cnt, dec_cbbase, dec_cboff, dec_nblk, dec_segbase, dec_fo;
+    DevBuf<int16_t> dec_pcm;
+    DevBuf<double> dec_fpcm;
     int64_t chunk_blocks = 32768;
     int dbg = 0;                           // PAC_DEBUG_FLAGS (diagnostic builds of the timing only)
     // timing
@@ -239,6 +248,10 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->st_cursor.release();
     c->m_src_off.release(); c->m_dst_off.release(); c->m_size.release(); c->m_stage.release();
+    c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
+    c->dec_ov.release(); c->dec_lrms.release(); c->dec_codes.release(); c->dec_so.release();
+    c->dec_cnt.release(); c->dec_cbbase.release(); c->dec_cboff.release(); c->dec_nblk.release();
+    c->dec_segbase.release(); c->dec_fo.release(); c->dec_pcm.release(); c->dec_fpcm.release();
     c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release(); c->prof.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
@@ -312,6 +325,7 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
         free(h);
         return set_err(PAC_E_NOMEM, "device huffman tables");
     }
+    int rc2;
     hipError_t e = hipMemcpy(c->huff, h, sizeof(PacHuffTables), hipMemcpyHostToDevice);
     free(c->huff_host);
     c->huff_host = h;    // kept for pac_encode_block's field reconstruction
@@ -322,6 +336,44 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
         c->huff_dec[t][((uint64_t)h->esc_len[t] << 32) | h->esc_bits[t]] = -1;
     }
     if (e != hipSuccess) return set_err(PAC_E_HIP, "huffman upload: %s", hipGetErrorString(e));
+    // decoding tables (Huffman.decodeData, Huffman.py:321-344): level 1 on the
+    // first min(11, maxlen) bits, level 2 for longer codes
+    std::vector<uint32_t> tab;
+    for (int t = 0; t < PAC_NTAB; t++) {
+        int ml = h->esc_len[t];
+        for (int sym = 0; sym < PAC_NSYM; sym++) ml = std::max(ml, (int)h->len[t][sym]);
+        if (ml > 30) return set_err(PAC_E_TABLES, "code longer than 30 bits");
+        const int l1 = std::min(ml, 11), l2 = ml - l1;
+        const size_t base = tab.size();
+        tab.resize(base + ((size_t)1 << l1), 0u);
+        for (int sym = -1; sym < PAC_NSYM; sym++) {
+            const int len = sym < 0 ? h->esc_len[t] : h->len[t][sym];
+            if (!len) continue;
+            const uint32_t code = sym < 0 ? h->esc_bits[t] : h->bits[t][sym];
+            const uint32_t ent = ((uint32_t)len << 16) | (sym < 0 ? 0xffffu : (uint32_t)sym);
+            if (len <= l1) {
+                const uint32_t first = code << (l1 - len), n = 1u << (l1 - len);
+                for (uint32_t i = 0; i < n; i++) tab[base + first + i] = ent;
+            } else {
+                const uint32_t top = code >> (len - l1);
+                uint32_t& slot = tab[base + top];
+                if (!(slot >> 31)) {
+                    const size_t sub = tab.size();
+                    tab.resize(sub + ((size_t)1 << l2), 0u);
+                    tab[base + top] = 0x80000000u | (uint32_t)sub;
+                }
+                const size_t sub = tab[base + top] & 0x7fffffffu;
+                const uint32_t rest = code & ((1u << (len - l1)) - 1u);
+                const uint32_t first = rest << (ml - len), n = 1u << (ml - len);
+                for (uint32_t i = 0; i < n; i++) tab[sub + first + i] = ent;
+            }
+        }
+        c->hdec.base[t] = (int32_t)base;
+        c->hdec.maxlen[t] = ml;
+        c->hdec.l1[t] = l1;
+    }
+    if ((rc2 = c->hdec_tab.ensure(tab.size()))) return rc2;
+    HIPCHK(hipMemcpy(c->hdec_tab.p, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->have_huff = true;
     return PAC_OK;
 }
@@ -910,5 +962,131 @@ extern "C" int pac_set_chunk_blocks(pac_ctx* c, int64_t blocks) {
 extern "C" int pac_last_timing(pac_ctx* c, pac_timing* out) {
     if (!c || !out) return set_err(PAC_E_ARG, "null argument");
     *out = c->last;
+    return PAC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decoder
+// ---------------------------------------------------------------------------
+
+extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_streams, const uint8_t* data,
+                                  const int64_t* stream_byte_offsets, int32_t data_is_device, int32_t preroll,
+                                  int16_t* pcm_out, int64_t pcm_capacity_frames, int32_t pcm_is_device,
+                                  double* float_out, int64_t* frame_offsets) {
+    int rc;
+    if (!c || !p || !stream_byte_offsets || !frame_offsets || n_streams < 1)
+        return set_err(PAC_E_ARG, "null argument or n_streams < 1");
+    if ((rc = check_params(p))) return rc;
+    const bool master = p->profile == PAC_PROFILE_MASTER;
+    const int nch = p->n_channels;
+    if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
+    if (master && nch != 2) return set_err(PAC_E_UNSUPPORTED, "master profile is stereo");
+    if (stream_byte_offsets[0] != 0) return set_err(PAC_E_ARG, "stream_byte_offsets[0] must be 0");
+    for (int s = 0; s < n_streams; s++)
+        if (stream_byte_offsets[s + 1] < stream_byte_offsets[s])
+            return set_err(PAC_E_ARG, "stream_byte_offsets must be non-decreasing");
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    hipStream_t s = c->stream;
+    const int64_t nbytes = stream_byte_offsets[n_streams];
+    const uint8_t* ddev = data;
+    if (!data_is_device) {
+        if ((rc = c->dec_data.ensure(nbytes + 8))) return rc;
+        if (nbytes) HIPCHK(hipMemcpyAsync(c->dec_data.p, data, nbytes, hipMemcpyHostToDevice, s));
+        ddev = c->dec_data.p;
+    }
+    if ((rc = c->dec_so.ensure(n_streams + 1)) || (rc = c->dec_cnt.ensure(n_streams)) ||
+        (rc = c->dec_cbbase.ensure(n_streams + 1)) || (rc = c->dec_nblk.ensure(n_streams)) ||
+        (rc = c->dec_segbase.ensure(n_streams + 1)) || (rc = c->dec_fo.ensure(n_streams + 1)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(c->dec_so.p, stream_byte_offsets, (n_streams + 1) * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_dec_count, dim3((n_streams + 255) / 256), dim3(256), 0, s, ddev, c->dec_so.p, n_streams,
+                       c->dec_cnt.p);
+    HIPCHK(hipGetLastError());
+    std::vector<int64_t> cnt(n_streams), cbb(n_streams + 1), nb(n_streams), segb(n_streams + 1);
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->dec_cnt.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int64_t G = 0, segs = 0, frames = 0;
+    for (int k = 0; k < n_streams; k++) {
+        if (cnt[k] < 0 || cnt[k] % nch)
+            return set_err(PAC_E_ARG, "stream %d: malformed data section (channel-blocks %lld, %d channels)", k,
+                           (long long)cnt[k], nch);
+        cbb[k] = G;
+        G += cnt[k];
+        nb[k] = cnt[k] / nch;
+        segb[k] = segs;
+        segs += (nb[k] + DEC_SEG - 1) / DEC_SEG;
+        frame_offsets[k] = frames;
+        frames += (nb[k] + (preroll ? 1 : 0)) * PAC_HALFN;
+    }
+    cbb[n_streams] = G;
+    segb[n_streams] = segs;
+    frame_offsets[n_streams] = frames;
+    if (!pcm_out || pcm_capacity_frames < frames)
+        return set_err(PAC_E_CAPACITY, "decoded output needs %lld frames, capacity %lld", (long long)frames,
+                       (long long)pcm_capacity_frames);
+    if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
+    const int64_t G1 = G > 0 ? G : 1;
+    if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(G1 * PAC_HALFN)) ||
+        (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
+        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(c->dec_cbbase.p, cbb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->dec_nblk.p, nb.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->dec_segbase.p, segb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
+                          s));
+    HIPCHK(hipMemcpyAsync(c->dec_fo.p, frame_offsets, (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    int16_t* pdev = pcm_out;
+    if (!pcm_is_device) {
+        if ((rc = c->dec_pcm.ensure(frames * nch + 1))) return rc;
+        pdev = c->dec_pcm.p;
+    }
+    double* fdev = nullptr;
+    if (float_out) {
+        if ((rc = c->dec_fpcm.ensure(frames * nch + 1))) return rc;
+        fdev = c->dec_fpcm.p;
+    }
+    // an empty data section still yields the one all-zero ReadDataBlock result with preroll
+    if (preroll)
+        for (int k = 0; k < n_streams; k++)
+            if (!nb[k]) {
+                HIPCHK(hipMemsetAsync(pdev + frame_offsets[k] * nch, 0, PAC_HALFN * nch * sizeof(int16_t), s));
+                if (fdev) HIPCHK(hipMemsetAsync(fdev + frame_offsets[k] * nch, 0, PAC_HALFN * nch * sizeof(double), s));
+            }
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
+    if (G) {
+        hipLaunchKernelGGL(k_dec_index, dim3((n_streams + 255) / 256), dim3(256), 0, s, ddev, c->dec_so.p, n_streams,
+                           c->dec_cbbase.p, c->dec_cboff.p);
+        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p};
+        hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, ddev, c->dec_cboff.p, G,
+                           (int)master, T, master ? c->hdec_tab.p : nullptr, c->hdec, D);
+        HIPCHK(hipGetLastError());
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+        PacDecOut O{pdev, fdev, c->dec_fo.p, preroll ? 1 : 0};
+        const int64_t grid = segs * (master ? 1 : nch);
+        if (grid > 0)
+            hipLaunchKernelGGL(k_dec_synth, dim3((unsigned)grid), dim3(256), 0, s, T, D, c->dec_cbbase.p,
+                               c->dec_nblk.p, c->dec_segbase.p, n_streams, nch, (int)master, O);
+        HIPCHK(hipGetLastError());
+    } else if (c->timing) {
+        HIPCHK(hipEventRecord(c->ev[1], s));
+    }
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
+    if (!pcm_is_device && frames)
+        HIPCHK(hipMemcpyAsync(pcm_out, pdev, frames * nch * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+    if (float_out && frames)
+        HIPCHK(hipMemcpyAsync(float_out, fdev, frames * nch * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (c->timing) {
+        hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);    // parse
+        hipEventElapsedTime(&c->last.pack_ms, c->ev[1], c->ev[2]);     // synthesis
+        c->last.alloc_ms = 0;
+        c->last.scan_ms = 0;
+        hipEventElapsedTime(&c->last.total_ms, c->ev[0], c->ev[2]);
+        c->last.n_channel_blocks = G;
+        c->last.out_bytes = frames * nch * 2;
+    }
     return PAC_OK;
 }

@@ -1,0 +1,271 @@
+// pac_decode.hip -- gfx950 kernels of the PAC/WAK decoder:
+// PACFile.ReadDataBlock (codec/pacfile.py:153-229, Origin pacfile.py
+// ReadDataBlock), Huffman.decodeData (Huffman.py:321-344), codec.Decode
+// (codec.py:25-65, Origin codec.py Decode) with vDequantize
+// (quantize.py:345-376), IMDCT (mdct.py:72-79), SineWindow, the overlap-add
+// and the decode driver's block order (pacfile.py:478-499), and
+// PCMFile.WriteDataBlock's sample conversion (pcmfile.py:118-147).
+//
+//   k_dec_count / k_dec_index  one thread per stream: walk the '<L nBytes'
+//                              prefixes -> channel-block offsets
+//   k_dec_parse                one LANE per channel-block: the serial bit
+//                              parse (band headers, raw mantissas or sign bits
+//                              + two-level table Huffman decode, LRMS)
+//   k_dec_synth                256 threads per (stream, run of 16 blocks
+//                              [, channel]): dequantize, M/S with the
+//                              reference's channel aliasing, IMDCT (DCT-IV via
+//                              the 512-point Stockham FFT), sine window,
+//                              overlap-add, int16 conversion
+#include "pac_wave.h"
+#include "pac_kernels.h"
+
+// Two-level Huffman decoding tables (built on the host in pac_huffman_load):
+// level 1 indexed by the first l1 bits of the next maxlen bits; an entry is
+// (len << 16) | symbol, symbol 0xFFFF = the escape code, or 0x80000000 | the
+// offset of a level-2 table indexed by the remaining maxlen - l1 bits.
+struct PacHuffDec {
+    int32_t base[PAC_NTAB];
+    int32_t maxlen[PAC_NTAB];
+    int32_t l1[PAC_NTAB];
+};
+
+#define DEC_SEG 16      // blocks per synthesis workgroup
+
+__global__ void k_dec_count(const uint8_t* __restrict__ data, const int64_t* __restrict__ so, int n,
+                            int64_t* __restrict__ cnt) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    int64_t pos = so[s], c = 0;
+    const int64_t end = so[s + 1];
+    while (pos + 4 <= end) {
+        const uint8_t* p = data + pos;
+        const uint32_t nb = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+        pos += 4 + (int64_t)nb;
+        c++;
+    }
+    cnt[s] = pos == end ? c : -1;     // -1: the last channel-block runs past the stream
+}
+
+__global__ void k_dec_index(const uint8_t* __restrict__ data, const int64_t* __restrict__ so, int n,
+                            const int64_t* __restrict__ cb_base, int64_t* __restrict__ cb_off) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    int64_t pos = so[s], g = cb_base[s];
+    const int64_t end = so[s + 1];
+    while (pos + 4 <= end) {
+        const uint8_t* p = data + pos;
+        const uint32_t nb = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+        cb_off[g++] = pos;
+        pos += 4 + (int64_t)nb;
+    }
+}
+
+// MSB-first bit reader over one channel-block's nBytes (bytes past the end
+// read as 0, as PackedBits would never be asked for them in a valid stream)
+struct DecBits {
+    const uint8_t* p;
+    int64_t n, bit;
+    __device__ __forceinline__ uint8_t byte(int64_t i) const { return i < n ? p[i] : 0; }
+    __device__ __forceinline__ uint32_t peek32() const {
+        const int64_t i = bit >> 3;
+        const uint64_t w = ((uint64_t)byte(i) << 32) | ((uint64_t)byte(i + 1) << 24) |
+                           ((uint64_t)byte(i + 2) << 16) | ((uint64_t)byte(i + 3) << 8) | byte(i + 4);
+        return (uint32_t)((w << (24 + (bit & 7))) >> 32);
+    }
+    __device__ __forceinline__ uint32_t read(int nb) {
+        if (nb <= 0) return 0;
+        const uint32_t v = peek32() >> (32 - nb);
+        bit += nb;
+        return v;
+    }
+};
+
+__device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restrict__ tab, const PacHuffDec& hd,
+                                             int id, int ba) {
+    const int ml = hd.maxlen[id], l1 = hd.l1[id];
+    const uint32_t idx = r.peek32() >> (32 - ml);
+    uint32_t e = tab[hd.base[id] + (idx >> (ml - l1))];
+    if (e >> 31) e = tab[(e & 0x7fffffffu) + (idx & ((1u << (ml - l1)) - 1u))];
+    int len = (e >> 16) & 31;
+    uint32_t sym = e & 0xffffu;
+    if (!len) { len = 1; sym = 0; }         // not a code of the table: malformed input
+    r.bit += len;
+    return sym == 0xffffu ? r.read(ba) : sym;   // escape: the raw ba-bit symbol follows
+}
+
+// Per-channel-block fields: codes [G][1024] (signed mantissa codes as the
+// reference's ReadDataBlock builds them), ba/sf [G][25], overall [G],
+// lrms [G][25] (master).
+struct PacDecWork {
+    uint16_t* codes;
+    uint8_t* ba;
+    uint8_t* sf;
+    uint8_t* overall;
+    uint8_t* lrms;
+};
+
+__global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ data,
+                                                   const int64_t* __restrict__ cb_off, int64_t G, int master,
+                                                   const PacTables* __restrict__ T,
+                                                   const uint32_t* __restrict__ htab, PacHuffDec hd,
+                                                   PacDecWork D) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const uint8_t* p = data + cb_off[g];
+    DecBits r{p + 4, (int64_t)(p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)), 0};
+    D.overall[g] = (uint8_t)r.read(4);
+    const int id = master ? (int)r.read(4) - 1 : 0;
+    uint16_t* codes = D.codes + g * PAC_HALFN;
+    for (int b = 0; b < PAC_NB; ++b) {
+        int a = (int)r.read(4);
+        if (a) a++;
+        D.ba[g * PAC_NB + b] = (uint8_t)a;
+        D.sf[g * PAC_NB + b] = (uint8_t)r.read(4);
+        if (!a) continue;
+        const int lo = T->lower[b], nl = T->nlines[b];
+        if (!master) {
+            for (int l = lo; l < lo + nl; ++l) codes[l] = (uint16_t)r.read(a);
+        } else {
+            const int64_t sbit = r.bit;           // nl sign bits, then nl Huffman codes
+            r.bit += nl;
+            const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
+            for (int l = lo; l < lo + nl; ++l) {
+                const uint32_t sym = dec_huff(r, htab, hd, tid, a);
+                DecBits sr{r.p, r.n, sbit + (l - lo)};
+                codes[l] = (uint16_t)(sym + (sr.read(1) << (a - 1)));
+            }
+        }
+    }
+    if (master)
+        for (int b = 0; b < PAC_NB; ++b) D.lrms[g * PAC_NB + b] = (uint8_t)r.read(1);
+}
+
+// vDequantize (quantize.py:345-376) + vDequantizeUniform (:118-145), 4 scale bits
+__device__ __forceinline__ double pac_dequantize(int scale, int64_t m, int ba) {
+    const int64_t smask = (int64_t)1 << (ba - 1);
+    const bool neg = (m & smask) == smask;
+    if (neg) m -= smask;
+    int64_t q = m << (15 - scale);
+    if (scale < 15 && m > 0) q += (int64_t)1 << (14 - scale);
+    const int64_t sm = (int64_t)1 << (ba + 14);
+    const double largest = (double)(sm << 1) - 1.0;
+    const double a = (2.0 * (double)q) / largest;
+    return neg ? -a : a;
+}
+
+// PCMFile.WriteDataBlock: sign, vQuantizeUniform(|x|, 16), re-sign
+__device__ __forceinline__ int16_t pac_float_to_pcm(double x) {
+    const bool s = __builtin_signbit(x);
+    const double a = s ? -x : x;
+    const uint64_t code = a < 1.0 ? (uint64_t)((a * 65535.0 + 1.0) / 2.0) : 32767u;
+    const int16_t c = (int16_t)code;
+    return s ? (int16_t)-c : c;
+}
+
+// dequantized lines of channel-block g into L (LDS), / 2^overall
+template <int NT>
+__device__ __forceinline__ void grp_dequant(const PacTables* __restrict__ T, const PacDecWork& D, int64_t g,
+                                            double* L, int tid) {
+    const int ov = D.overall[g];
+    const double rescale = 1.0 * (double)(1 << ov);
+#pragma unroll
+    for (int i = 0; i < PAC_HALFN / NT; ++i) {
+        const int l = i * NT + tid;
+        const int b = T->band_of_line[l];
+        const int ba = (l < T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1]) ? D.ba[g * PAC_NB + b] : 0;
+        double v = 0.0;
+        if (ba) v = pac_dequantize(D.sf[g * PAC_NB + b], D.codes[g * PAC_HALFN + l], ba);
+        L[l] = v / rescale;
+    }
+}
+
+// IMDCT (mdct.py:72-79) of the lines in L, sine-windowed: w(n) for n < 2048
+// from U = 2 DCT-IV(L) (in buf):  n < 512: U[n+512];  512 <= n < 1536:
+// -U[1535-n];  n >= 1536: -U[n-1536]
+__device__ __forceinline__ double imdct_window_at(const double* U, const PacTables* __restrict__ T, int n) {
+    const double y = n < 512 ? U[n + 512] : (n < 1536 ? -U[1535 - n] : -U[n - 1536]);
+    return y * T->sine[n];
+}
+
+// one synthesis workgroup: blocks [b0, b1) of stream s, channels c0 .. c0+nc-1
+// (nc = 1 origin, 2 master), output frames of ReadDataBlock results
+// ob = b - 1 (b >= 1; result 0 is the one the driver skips) or, with preroll,
+// ob = b; plus the final overlap half when b1 is the stream's last block.
+struct PacDecOut {
+    int16_t* pcm;          // interleaved [frames][nch]
+    double* fpcm;          // optional float64 samples, same layout
+    const int64_t* fo;     // [n_streams] first output frame of each stream
+    int preroll;
+};
+
+__global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__ T, PacDecWork D,
+                                                   const int64_t* __restrict__ cb_base,
+                                                   const int64_t* __restrict__ nblk,
+                                                   const int64_t* __restrict__ seg_base, int n_streams,
+                                                   int nch, int master, PacDecOut O) {
+    __shared__ double2 buf[1024];                 // IMDCT scratch
+    __shared__ double lines[2][PAC_HALFN];
+    __shared__ double prev[2][PAC_HALFN];
+    const int tid = threadIdx.x;
+    const int nc = master ? 2 : 1;
+    const int64_t item = blockIdx.x / (master ? 1 : nch);
+    const int c0 = master ? 0 : (int)(blockIdx.x % nch);
+    // stream of this segment: last s with seg_base[s] <= item
+    int lo = 0, hi = n_streams;
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (seg_base[mid] <= item) lo = mid; else hi = mid; }
+    const int s = lo;
+    const int64_t nb = nblk[s];
+    const int64_t b0 = (item - seg_base[s]) * DEC_SEG;
+    const int64_t b1 = b0 + DEC_SEG < nb ? b0 + DEC_SEG : nb;
+    const int64_t first_out = O.preroll ? 0 : 1;
+    for (int c = 0; c < nc; ++c)
+        for (int i = tid; i < PAC_HALFN; i += 256) prev[c][i] = 0.0;
+    __syncthreads();
+    for (int64_t b = b0 > 0 ? b0 - 1 : 0; b < b1; ++b) {
+        for (int c = 0; c < nc; ++c)
+            grp_dequant<256>(T, D, cb_base[s] + b * nch + c0 + c, lines[c], tid);
+        __syncthreads();
+        if (master) {
+            // codec.py:46-54: mdctLineL/R alias mdctLine[0]/[1]; the second
+            // assignment reads the updated channel 0: L = M - S, R = (M - S) + S
+            const uint8_t* lr = D.lrms + (cb_base[s] + b * nch + 1) * PAC_NB;   // last channel's bits
+#pragma unroll
+            for (int i = 0; i < PAC_HALFN / 256; ++i) {
+                const int l = i * 256 + tid;
+                if (l < T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1] && lr[T->band_of_line[l]]) {
+                    const double a = lines[0][l] - lines[1][l];
+                    lines[0][l] = a;
+                    lines[1][l] = a + lines[1][l];
+                }
+            }
+            __syncthreads();
+        }
+        for (int c = 0; c < nc; ++c) {
+            const double* U = grp_dct4<256>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
+            const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
+#pragma unroll
+            for (int i0 = 0; i0 < PAC_HALFN; i0 += 256) {
+                const int i = i0 + tid;
+                const double w0 = imdct_window_at(U, T, i), w1 = imdct_window_at(U, T, i + PAC_HALFN);
+                if (b >= b0 && b >= 1 - (O.preroll ? 1 : 0)) {
+                    const double v = prev[c][i] + w0;
+                    const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
+                    O.pcm[o] = pac_float_to_pcm(v);
+                    if (O.fpcm) O.fpcm[o] = v;
+                }
+                prev[c][i] = w1;
+            }
+            __syncthreads();      // U (buf) is rewritten by the next channel / block
+        }
+    }
+    if (b1 == nb && nb > 0) {        // end of file: the saved half alone
+        const int64_t ob = nb - 1 + (O.preroll ? 1 : 0);
+        for (int c = 0; c < nc; ++c)
+            for (int i = tid; i < PAC_HALFN; i += 256) {
+                const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
+                O.pcm[o] = pac_float_to_pcm(prev[c][i]);
+                if (O.fpcm) O.fpcm[o] = prev[c][i];
+            }
+    }
+    (void)first_out;
+}

@@ -170,38 +170,49 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
     return src;
 }
 
-// MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
-// sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
-// place in codec.py:240).  Evaluated as DCT-IV of the folded block with a
-// 512-point complex Stockham FFT.  buf: 1024 double2 of LDS.  Output: the
-// 1024 lines as doubles in the first 8 KB of buf (X = (double*)buf); the
-// second 8 KB is free scratch on return.  An exactly-zero line keeps the
-// reference's sign (mdct_zero_neg).
-template <int NT, class XS>
-__device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __restrict__ T,
-                                            double2* buf, int tid) {
+// DCT-IV of 1024 values v(j), scaled by sc (a power of two):
+//   X[k] = sc * sum_j v(j) cos(pi/1024 (j + 1/2)(k + 1/2)),
+// via the 512-point complex Stockham FFT (even/odd interleave, pre- and
+// post-twiddles).  buf: 1024 double2 of LDS; X = (double*)buf on return (first
+// 8 KB), the second 8 KB is free scratch.
+template <int NT, class V>
+__device__ __forceinline__ double* grp_dct4(const V& v, const PacTables* __restrict__ T, double2* buf, int tid,
+                                            double sc) {
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
-        int q = q0 + tid;
-        int n0 = 2 * q, n1 = 1023 - 2 * q;
-        // fold [a b c d] -> (-c_r - d, a - b_r)
-        double u0 = n0 < 512 ? __dsub_rn(-xs(1535 - n0), xs(1536 + n0))
-                             : __dsub_rn(xs(n0 - 512), xs(1535 - n0));
-        double u1 = n1 < 512 ? __dsub_rn(-xs(1535 - n1), xs(1536 + n1))
-                             : __dsub_rn(xs(n1 - 512), xs(1535 - n1));
-        buf[q] = cmul(make_double2(u0, u1), T->mdct_pre[q]);
+        const int q = q0 + tid;
+        buf[q] = cmul(make_double2(v(2 * q), v(1023 - 2 * q)), T->mdct_pre[q]);
     }
     const double2* Y = grp_fft_stockham<9, NT>(buf, buf + 512, T->fft_tw, tid);   // = buf + 512
     double* X = reinterpret_cast<double*>(buf);
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
-        int q = q0 + tid;
-        double2 y = cmul(Y[q], T->mdct_post[q]);
-        double x0 = y.x * (1.0 / 1024.0), x1 = -y.y * (1.0 / 1024.0);
-        if (x0 == 0.0) x0 = T->mdct_zero_neg[2 * q] ? -0.0 : 0.0;
-        if (x1 == 0.0) x1 = T->mdct_zero_neg[1023 - 2 * q] ? -0.0 : 0.0;
-        X[2 * q] = x0;
-        X[1023 - 2 * q] = x1;
+        const int q = q0 + tid;
+        const double2 y = cmul(Y[q], T->mdct_post[q]);
+        X[2 * q] = y.x * sc;
+        X[1023 - 2 * q] = -y.y * sc;
+    }
+    grp_sync<NT>();
+    return X;
+}
+
+// MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
+// sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
+// place in codec.py:240): the DCT-IV of the folded block [a b c d] ->
+// (-c_r - d, a - b_r), times 1/1024.  buf: 1024 double2 of LDS.  Output: the
+// 1024 lines as doubles in the first 8 KB of buf (X = (double*)buf).  An
+// exactly-zero line keeps the reference's sign (mdct_zero_neg).
+template <int NT, class XS>
+__device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __restrict__ T,
+                                            double2* buf, int tid) {
+    auto fold = [&](int n) {
+        return n < 512 ? __dsub_rn(-xs(1535 - n), xs(1536 + n)) : __dsub_rn(xs(n - 512), xs(1535 - n));
+    };
+    double* X = grp_dct4<NT>(fold, T, buf, tid, 1.0 / 1024.0);
+#pragma unroll
+    for (int k0 = 0; k0 < 1024; k0 += NT) {
+        const int k = k0 + tid;
+        if (X[k] == 0.0) X[k] = T->mdct_zero_neg[k] ? -0.0 : 0.0;
     }
     grp_sync<NT>();
     return X;

@@ -10,7 +10,11 @@ WriteDataBlock / Close / Encode) and file layout:
 Every block is encoded by the HIP kernels (``codec.Encode`` ->
 ``pac_encode_block``).  For throughput use the batch entry points
 ``encode_file`` / ``encode_streams`` which run whole streams in one GPU call
-(``pac_encode_streams``); the bytes are identical.
+(``pac_encode_streams``); the bytes are identical.  Decoding
+(``ReadDataBlock``, ``decode_file``, ``decode_streams``) runs on the GPU
+through ``pac_decode_streams``: the file's data section is decoded in one call
+when it is opened and ReadDataBlock hands out the reference's per-block
+results (overlap-added signed fractions, then the final overlap half).
 """
 import struct
 
@@ -71,7 +75,21 @@ class PACFile(AudioFile):
         return p
 
     def ReadDataBlock(self, codingParams, huffman=None):
-        raise NotImplementedError("decoder path is the next row of SURVEY.md 8(f)")
+        """pacfile.py:153-229: the next block of reconstituted signed-fraction
+        samples per channel (1024 each), the final overlap-and-add half at the
+        end of the file, then None."""
+        if getattr(self, "_dec", None) is None:
+            data = self.fp.read()
+            ctx = self.context or codec.default_context()
+            p = _lib.params(codingParams.sampleRate, codingParams.nChannels, self.profile)
+            _, fo, fl = ctx.decode_streams(p, data, [0, len(data)], preroll=True, want_float=True)
+            self._dec = fl
+            self._pos = 0
+        if self._pos >= self._dec.shape[0]:
+            return None
+        blk = self._dec[self._pos:self._pos + codingParams.nMDCTLines]
+        self._pos += codingParams.nMDCTLines
+        return [blk[:, c].copy() for c in range(codingParams.nChannels)]
 
     def WriteFileHeader(self, codingParams):
         self.fp.write(header_bytes(codingParams.sampleRate, codingParams.nChannels,
@@ -133,3 +151,54 @@ def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):
         with open(out_path, "wb") as f:
             f.write(data)
     return data
+
+
+# ---------------------------------------------------------------------------
+# decoding (pacfile.py:153-229, codec.py:25-65, the driver pacfile.py:478-499)
+# ---------------------------------------------------------------------------
+
+def parse_header(b):
+    """PACFile.ReadFileHeader on bytes: (sampleRate, nChannels, numSamples,
+    nLines, offset of the data section)"""
+    if b[:4] != PACFile.tag:
+        raise ValueError("Tried to read a non-PAC file into a PACFile object")
+    fs, nch, ns, nmdct, nsb, nmb = struct.unpack("<LHLLHH", b[4:22])
+    nb = struct.unpack("<L", b[22:26])[0]
+    nl = struct.unpack("<%dH" % nb, b[26:26 + 2 * nb])
+    return fs, nch, ns, list(nl), 26 + 2 * nb
+
+
+def decode_streams(sections, sample_rate, n_channels, profile=PROFILE_MASTER, context=None, preroll=False):
+    """Decode independent data sections (bytes) sharing sample rate and channel
+    count in one GPU call.  Returns a list of int16 [frames, nCh] arrays: the
+    frames the reference's decode driver writes (or, with preroll, every
+    ReadDataBlock result)."""
+    ctx = context or codec.default_context()
+    so = np.zeros(len(sections) + 1, dtype=np.int64)
+    so[1:] = np.cumsum([len(x) for x in sections])
+    p = _lib.params(sample_rate, n_channels, profile)
+    pcm, fo, _ = ctx.decode_streams(p, b"".join(sections), so, preroll=preroll)
+    return [pcm[fo[i]:fo[i + 1]] for i in range(len(sections))]
+
+
+def wav_bytes(sampleRate, nChannels, numSamples, frames):
+    """PCMFile.WriteFileHeader (sizes from numSamples, pcmfile.py:103-116)
+    followed by the frames, as the reference decode driver writes them"""
+    data_bytes = numSamples * nChannels * 2
+    h = struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + data_bytes, b"WAVE", b"fmt ", 16, 1, nChannels,
+                    sampleRate, sampleRate * nChannels * 2, nChannels * 2, 16, b"data", data_bytes)
+    return h + np.ascontiguousarray(frames, dtype="<i2").tobytes()
+
+
+def decode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):
+    """The reference driver's decode half (pacfile.py:430-499) for one coded
+    file, as one GPU call.  Returns the output WAV bytes (and writes them)."""
+    with open(in_path, "rb") as f:
+        b = f.read()
+    fs, nch, ns, _, off = parse_header(b)
+    pcm = decode_streams([b[off:]], fs, nch, profile, context)[0]
+    out = wav_bytes(fs, nch, ns, pcm)
+    if out_path:
+        with open(out_path, "wb") as f:
+            f.write(out)
+    return out

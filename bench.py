@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=["encode", "decode"], default="encode",
+                    help="encode = the metric (default); decode = pac_decode_streams of the same "
+                         "workload's bitstream (encoded once, untimed)")
     ap.add_argument("--profile", choices=["origin", "master"], default="origin",
                     help="origin = BASELINE configs[1] (white noise, M/S off, the metric's config); "
                          "master = configs[2] (pink noise + tones, M/S + Huffman)")
@@ -190,6 +193,110 @@ def parity_check(ctx, out_dev, so, oracle_prefixes):
             "against": "oracle/pac_oracle.c on the CPU-baseline sample"}
 
 
+def bench_decode(a, dist, ctx, p, encode_step, out_dev, ns, blocks, master):
+    """Decoder throughput: the workload's bitstream (encoded once on the GPU,
+    untimed) decoded by pac_decode_streams with input and output in HBM."""
+    _, so = encode_step()
+    frames = blocks * 1024
+    pcm_out = ctx.alloc(frames * 2 * 2)
+
+    def step():
+        return ctx.decode_streams(p, out_dev, so, data_is_device=True, out=pcm_out,
+                                  out_capacity_frames=frames, out_is_device=True)
+
+    for _ in range(a.warmup):
+        step()
+    parse_ms, synth_ms = [], []
+    dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _, fo, _ = step()
+        t = ctx.last_timing()
+        parse_ms.append(t.front_ms)
+        synth_ms.append(t.pack_ms)
+    ctx.sync()
+    dist.barrier()
+    el_max = dist.max(time.perf_counter() - t0)
+    total_blocks = dist.sum(blocks)
+    in_bytes = int(so[-1])
+    # algorithmic bytes per launch of the decode path: the bitstream read once
+    # + int16 PCM written once
+    dec_s = (float(np.mean(parse_ms)) + float(np.mean(synth_ms))) / 1e3
+    alg = in_bytes + frames * 4
+    res = {
+        "metric": "stereo 1024-sample blocks decoded/s",
+        "value": total_blocks / (el_max / a.steps),
+        "unit": "blocks/s",
+        "n_gpus": dist.world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": el_max / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic, encoded on the GPU from %s" % ("pink noise + tones" if master else "white noise"),
+        "config": {"workload": "decode of the %s workload's bitstream (%d stereo blocks per GPU)"
+                               % ("configs[2]" if master else "configs[1]", blocks),
+                   "profile": a.profile, "streams_per_gpu": ns, "blocks_per_stream": a.blocks_per_stream,
+                   "global_blocks": int(total_blocks),
+                   "parallelism": "streams sharded, %d rank(s)" % dist.world},
+        "roofline": {"bound": "hbm", "kernel": "k_dec_parse + k_dec_synth", "achieved": alg / dec_s / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / dec_s / 1e9 / HBM_PEAK_GBS,
+                     "traffic": None},
+        "kernels_ms": {"parse": float(np.mean(parse_ms)), "synth": float(np.mean(synth_ms))},
+        "bitstream_bytes_per_gpu": in_bytes,
+    }
+    if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
+        res["cpu_baseline"], res["parity"] = cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master)
+    ctx.free(pcm_out)
+    if dist.rank == 0:
+        print(json.dumps(res))
+    dist.close()
+
+
+def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master):
+    """The oracle's decoder on the first streams' bytes (one host thread per
+    stream, bounded), and its frames against the GPU's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as P
+    from concurrent.futures import ThreadPoolExecutor
+    P.lib()
+    threads = max(1, min(a.cpu_threads, len(so) - 1))
+    secs = []
+    for t in range(threads):
+        b = np.empty(int(so[t + 1] - so[t]), dtype=np.uint8)
+        ctx.to_host(b, out_dev + int(so[t]))
+        secs.append(b.tobytes())
+    t0 = time.perf_counter()
+
+    def work(t):
+        o = P.Oracle(a.sample_rate, huffman=master)
+        n = 0
+        ref = None
+        while time.perf_counter() - t0 < a.cpu_seconds or ref is None:
+            ref = o.decode_data(P.MASTER if master else P.ORIGIN, secs[t], 2)
+            n += ref.shape[0] // 1024
+        return n, ref
+
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(work, range(threads)))
+    el = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    checked = bad = 0
+    for t, (_, ref) in enumerate(res):
+        got = np.empty(ref.shape, dtype=np.int16)
+        ctx.to_host(got, pcm_out + int(fo[t]) * 4)
+        checked += ref.shape[0] // 1024
+        bad += int(np.sum(np.any((got != ref).reshape(-1, 1024 * 2), axis=1)))
+    base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
+            "sample": "oracle/pac_oracle.c decoder, %d host threads (one stream each), %d stereo blocks "
+                      "in %.1f s" % (threads, done, el)}
+    return base, {"checked_blocks": checked, "mismatching": bad,
+                  "against": "oracle/pac_oracle.c decoder on the CPU-baseline sample"}
+
+
 def main():
     a = parse()
     dist = Dist()
@@ -215,6 +322,9 @@ def main():
     def step():
         return ctx.encode_streams(p, pcm_dev, fo, out=out_dev, out_capacity=cap,
                                   pcm_is_device=True, out_is_device=True)
+
+    if a.mode == "decode":
+        return bench_decode(a, dist, ctx, p, step, out_dev, ns, blocks, master)
 
     for _ in range(a.warmup):
         step()

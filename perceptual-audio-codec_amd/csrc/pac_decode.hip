@@ -10,7 +10,8 @@
 //                              prefixes -> channel-block offsets
 //   k_dec_parse                one LANE per channel-block: the serial bit
 //                              parse (band headers, raw mantissas or sign bits
-//                              + two-level table Huffman decode, LRMS)
+//                              + two-level table Huffman decode, LRMS) from a
+//                              64-bit buffer refilled by aligned 32-bit loads
 //   k_dec_synth                256 threads per (stream, run of 16 blocks
 //                              [, channel]): dequantize, M/S with the
 //                              reference's channel aliasing, IMDCT (DCT-IV via
@@ -60,25 +61,57 @@ __global__ void k_dec_index(const uint8_t* __restrict__ data, const int64_t* __r
     }
 }
 
-// MSB-first bit reader over one channel-block's nBytes (bytes past the end
-// read as 0, as PackedBits would never be asked for them in a valid stream)
+// MSB-first bit reader over one channel-block's bytes: aligned 32-bit loads
+// into a 64-bit buffer (one load per 32 bits consumed).  It runs ahead by up
+// to two words, i.e. it may load up to 8 bytes past the channel-block (bits
+// it never consumes): host data is staged with 8 bytes of padding, device
+// buffers come from hipMalloc (page granular).
 struct DecBits {
-    const uint8_t* p;
-    int64_t n, bit;
-    __device__ __forceinline__ uint8_t byte(int64_t i) const { return i < n ? p[i] : 0; }
-    __device__ __forceinline__ uint32_t peek32() const {
-        const int64_t i = bit >> 3;
-        const uint64_t w = ((uint64_t)byte(i) << 32) | ((uint64_t)byte(i + 1) << 24) |
-                           ((uint64_t)byte(i + 2) << 16) | ((uint64_t)byte(i + 3) << 8) | byte(i + 4);
-        return (uint32_t)((w << (24 + (bit & 7))) >> 32);
+    const uint32_t* w;     // aligned word stream
+    uint64_t buf;          // next bits, MSB first
+    int nbuf;
+    __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
+    __device__ __forceinline__ void init(const uint8_t* p, int64_t bit0) {
+        const uintptr_t a = (uintptr_t)p + (uintptr_t)(bit0 >> 3);
+        w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const int skip = (int)((a & 3) * 8 + (bit0 & 7));
+        buf = (uint64_t)be(*w++) << 32;
+        nbuf = 32;
+        refill();
+        buf <<= skip;
+        nbuf -= skip;
+        refill();
     }
-    __device__ __forceinline__ uint32_t read(int nb) {
+    __device__ __forceinline__ void refill() {
+        if (nbuf <= 32) {
+            buf |= (uint64_t)be(*w++) << (32 - nbuf);
+            nbuf += 32;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek32() const { return (uint32_t)(buf >> 32); }
+    __device__ __forceinline__ void skip(int nb) {
+        buf <<= nb;
+        nbuf -= nb;
+        refill();
+    }
+    __device__ __forceinline__ void advance(int n) {      // any n >= 0
+        while (n > 32) { skip(32); n -= 32; }
+        skip(n);
+    }
+    __device__ __forceinline__ uint32_t read(int nb) {     // nb <= 32
         if (nb <= 0) return 0;
-        const uint32_t v = peek32() >> (32 - nb);
-        bit += nb;
+        const uint32_t v = (uint32_t)(buf >> (64 - nb));
+        skip(nb);
         return v;
     }
 };
+
+// bits consumed so far by reader r started at payload p, bit 0
+__device__ __forceinline__ int64_t bits_consumed(const DecBits& r, const uint8_t* p) {
+    const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)3;
+    const int64_t loaded = ((int64_t)((uintptr_t)r.w - a0)) * 8;     // bits loaded from a0
+    return loaded - r.nbuf - (int64_t)(((uintptr_t)p & 3) * 8);
+}
 
 __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restrict__ tab, const PacHuffDec& hd,
                                              int id, int ba) {
@@ -89,7 +122,7 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
     int len = (e >> 16) & 31;
     uint32_t sym = e & 0xffffu;
     if (!len) { len = 1; sym = 0; }         // not a code of the table: malformed input
-    r.bit += len;
+    r.skip(len);
     return sym == 0xffffu ? r.read(ba) : sym;   // escape: the raw ba-bit symbol follows
 }
 
@@ -112,29 +145,36 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint8_t* p = data + cb_off[g];
-    DecBits r{p + 4, (int64_t)(p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)), 0};
+    DecBits r;
+    r.init(p + 4, 0);
     D.overall[g] = (uint8_t)r.read(4);
     const int id = master ? (int)r.read(4) - 1 : 0;
     uint16_t* codes = D.codes + g * PAC_HALFN;
+    int64_t bit = master ? 8 : 4;         // bit position, for the sign-bit reader
     for (int b = 0; b < PAC_NB; ++b) {
         int a = (int)r.read(4);
         if (a) a++;
         D.ba[g * PAC_NB + b] = (uint8_t)a;
         D.sf[g * PAC_NB + b] = (uint8_t)r.read(4);
+        bit += 8;
         if (!a) continue;
         const int lo = T->lower[b], nl = T->nlines[b];
         if (!master) {
             for (int l = lo; l < lo + nl; ++l) codes[l] = (uint16_t)r.read(a);
+            bit += (int64_t)nl * a;
         } else {
-            const int64_t sbit = r.bit;           // nl sign bits, then nl Huffman codes
-            r.bit += nl;
+            DecBits sg;                            // nl sign bits, then nl Huffman codes
+            sg.init(p + 4, bit);
+            r.advance(nl);
+            bit += nl;
             const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
             for (int l = lo; l < lo + nl; ++l) {
                 const uint32_t sym = dec_huff(r, htab, hd, tid, a);
-                DecBits sr{r.p, r.n, sbit + (l - lo)};
-                codes[l] = (uint16_t)(sym + (sr.read(1) << (a - 1)));
+                codes[l] = (uint16_t)(sym + (sg.read(1) << (a - 1)));
             }
+            bit = -1;                              // recomputed below from the main reader
         }
+        if (bit < 0) bit = bits_consumed(r, p + 4);
     }
     if (master)
         for (int b = 0; b < PAC_NB; ++b) D.lrms[g * PAC_NB + b] = (uint8_t)r.read(1);

@@ -132,6 +132,31 @@ static void build_tables(int fs, PacTables* t) {
         t->peak_floor2 = m * m;
     }
     for (int i = 1; i < 64; i++) t->inv_int[i] = 1.0 / (double)i;
+    {   // numpy pairwise-sum leaves (loops_utils.h.src) of every band, in order
+        int nl = 0;
+        struct Rec {
+            static void go(PacTables* t, int& nl, int b, int e0, int n) {
+                if (n <= 128) {
+                    if (nl < 64) {
+                        t->lr_leaf_band[nl] = (int16_t)b;
+                        t->lr_leaf_e0[nl] = (int16_t)e0;
+                        t->lr_leaf_n[nl] = (int16_t)n;
+                    }
+                    nl++;
+                    return;
+                }
+                int n2 = n / 2;
+                n2 -= n2 % 8;
+                go(t, nl, b, e0, n2);
+                go(t, nl, b, e0 + n2 / 2, n - n2);
+            }
+        };
+        for (int b = 0; b < PAC_NB; b++) {
+            t->lr_first_leaf[b] = nl;
+            Rec::go(t, nl, b, 0, 2 * t->nlines[b]);
+        }
+        t->lr_nleaf = nl;     // <= 64 for any layout of 1024 lines (checked in get_tables)
+    }
     const int step = fs / PAC_N;  // Py2 integer division, psychoac.py:188
     double mx = -1.0;
     for (int k = 0; k < PAC_HALFN; k++) {
@@ -270,6 +295,10 @@ static int get_tables(pac_ctx* c, int fs, PacTables** out) {
     PacTables* h = (PacTables*)malloc(sizeof(PacTables));
     if (!h) return set_err(PAC_E_NOMEM, "host tables");
     build_tables(fs, h);
+    if (h->lr_nleaf > 64) {
+        free(h);
+        return set_err(PAC_E_UNSUPPORTED, "band layout of %d Hz needs more than 64 pairwise-sum leaves", fs);
+    }
     PacTables* d = nullptr;
     if (hipMalloc((void**)&d, sizeof(PacTables)) != hipSuccess) {
         free(h);
@@ -598,7 +627,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             const int64_t B = (int64_t)n_s * S;
             if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, ck);
-            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(64), 0, s, src, T, W, ck);
+            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s, src, T, W, ck);
             HIPCHK(hipGetLastError());
             if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
             hipLaunchKernelGGL(k_master_tail, dim3((unsigned)n_s), dim3(64), 0, s, T, c->huff, W, c->blk_off.p, ck,

@@ -39,6 +39,11 @@ struct PacTables {
     // the square of the largest double m with 10*log10(m) <= -30 (host libm)
     double peak_floor2;
     double inv_int[64];           // 1/i (inv_int[0] unused)
+    // leaves of numpy's pairwise complex sum over each band's FFT bins (the
+    // LRMS decision, codec.py:96-102): band, first element, length in doubles
+    int32_t lr_nleaf;
+    int32_t lr_first_leaf[PAC_NB];
+    int16_t lr_leaf_band[64], lr_leaf_e0[64], lr_leaf_n[64];
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

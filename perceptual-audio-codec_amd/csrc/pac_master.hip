@@ -101,179 +101,195 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
 }
 
 // --- numpy pairwise summation of a complex vector (loops_utils.h.src) -------
-// element j of the summed vector is f(j) (complex); n = 2 * count (doubles)
-template <int D, class F>
-__device__ double2 np_csum(const F& f, int e0, int n) {
+// np.sum over a band's complex values (n = 2 * count doubles): below 8
+// doubles a plain loop, up to 128 an 8-accumulator block, above that the sum
+// of the two halves split at (n/2) rounded down to a multiple of 8.  The
+// leaves of that recursion (PacTables::lr_leaf_*, host-built per band
+// layout) are summed one per lane; one lane per band then adds them in the
+// recursion's order.
+
+// leaf: doubles [0, n) of f(e0 + k), k < n/2
+template <class F>
+__device__ __forceinline__ double2 np_csum_leaf(const F& f, int e0, int n) {
     if (n < 8) {
         double sr = 0., si = 0.;
-        for (int i = 0; i < n; i += 2) { double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
+        for (int i = 0; i < n; i += 2) { const double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
         return make_double2(sr, si);
     }
-    if (D == 0 || n <= 128) {
-        double r[8];
-        double2 z0 = f(e0), z1 = f(e0 + 1), z2 = f(e0 + 2), z3 = f(e0 + 3);
-        r[0] = z0.x; r[1] = z0.y; r[2] = z1.x; r[3] = z1.y;
-        r[4] = z2.x; r[5] = z2.y; r[6] = z3.x; r[7] = z3.y;
-        int i;
-        for (i = 8; i < n - (n % 8); i += 8) {
-            int e = e0 + i / 2;
-            z0 = f(e); z1 = f(e + 1); z2 = f(e + 2); z3 = f(e + 3);
-            r[0] += z0.x; r[1] += z0.y; r[2] += z1.x; r[3] += z1.y;
-            r[4] += z2.x; r[5] += z2.y; r[6] += z3.x; r[7] += z3.y;
-        }
-        double sr = ((r[0] + r[2]) + (r[4] + r[6]));
-        double si = ((r[1] + r[3]) + (r[5] + r[7]));
-        for (; i < n; i += 2) { double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
-        return make_double2(sr, si);
+    double r[8];
+    double2 z0 = f(e0), z1 = f(e0 + 1), z2 = f(e0 + 2), z3 = f(e0 + 3);
+    r[0] = z0.x; r[1] = z0.y; r[2] = z1.x; r[3] = z1.y;
+    r[4] = z2.x; r[5] = z2.y; r[6] = z3.x; r[7] = z3.y;
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8) {
+        const int e = e0 + i / 2;
+        z0 = f(e); z1 = f(e + 1); z2 = f(e + 2); z3 = f(e + 3);
+        r[0] += z0.x; r[1] += z0.y; r[2] += z1.x; r[3] += z1.y;
+        r[4] += z2.x; r[5] += z2.y; r[6] += z3.x; r[7] += z3.y;
     }
+    double sr = ((r[0] + r[2]) + (r[4] + r[6]));
+    double si = ((r[1] + r[3]) + (r[5] + r[7]));
+    for (; i < n; i += 2) { const double2 z = f(e0 + i / 2); sr += z.x; si += z.y; }
+    return make_double2(sr, si);
+}
+
+// the recursion's combine step over precomputed leaf sums (in leaf order)
+template <int D>
+__device__ double2 np_csum_combine(const double2* leaf, int& idx, int n) {
+    if (D == 0 || n <= 128) return leaf[idx++];
     int n2 = n / 2;
     n2 -= n2 % 8;
-    double2 a = np_csum<(D > 0 ? D - 1 : 0)>(f, e0, n2);
-    double2 b = np_csum<(D > 0 ? D - 1 : 0)>(f, e0 + n2 / 2, n - n2);
+    const double2 a = np_csum_combine<(D > 0 ? D - 1 : 0)>(leaf, idx, n2);
+    const double2 b = np_csum_combine<(D > 0 ? D - 1 : 0)>(leaf, idx, n - n2);
     return make_double2(a.x + b.x, a.y + b.y);
 }
 
-// complex spectrum X[k], k < 1024, of a real 2048-block into buf (in place)
-template <class DS>
-__device__ __forceinline__ void wave_spectrum_cplx(const DS& d, const PacTables* __restrict__ T,
-                                                   double2* buf, int lane) {
+// complex spectrum X[k], k < 1024, of a real 2048-block d: staged in buf,
+// Stockham FFT into tmp, real split back into buf
+template <int NT, class DS>
+__device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* __restrict__ T, double2* buf,
+                                                  double2* tmp, int tid) {
 #pragma unroll 4
-    for (int n0 = 0; n0 < 1024; n0 += WAVE) {
-        int n = n0 + lane;
-        buf[brev(n, 10)] = make_double2(d(2 * n), d(2 * n + 1));
+    for (int n0 = 0; n0 < 1024; n0 += NT) {
+        const int n = n0 + tid;
+        buf[n] = make_double2(d(2 * n), d(2 * n + 1));
     }
-    wave_fft<10>(buf, T->fft_tw, lane);
+    const double2* Z = grp_fft_stockham<10, NT>(buf, tmp, T->fft_tw, tid);   // = tmp
 #pragma unroll
-    for (int t0 = 0; t0 <= 512; t0 += WAVE) {
-        int k = t0 + lane;
-        if (k > 512) continue;
-        int k2 = (1024 - k) & 1023;
-        double2 Za = buf[k], Zb = buf[k2];
-        double2 X[2];
+    for (int p0 = 0; p0 < 512; p0 += NT) {
+        const int p = p0 + tid;
+        int kk[2];
+        kk[0] = p;
+        kk[1] = p ? 1024 - p : 512;
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            int kk = side ? k2 : k;
-            double2 A = side ? Zb : Za;
-            double2 Bc = side ? Za : Zb;
-            double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
-            double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
-            double2 wo = cmul(T->rfft_tw[kk], o);
-            X[side] = make_double2(e.x + wo.y, e.y - wo.x);
+            const double2 A = Z[kk[side]];
+            const double2 Bc = Z[(1024 - kk[side]) & 1023];
+            const double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
+            const double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
+            const double2 wo = cmul(T->rfft_tw[kk[side]], o);
+            buf[kk[side]] = make_double2(e.x + wo.y, e.y - wo.x);
         }
-        buf[k] = X[0];
-        if (k2 != k) buf[k2] = X[1];
     }
-    wave_sync();
+    grp_sync<NT>();
 }
 
-__global__ __launch_bounds__(64) void k_master_front(PacSource src, const PacTables* __restrict__ T,
-                                                     PacMasterWork W, PacMasterChunk ck) {
-    __shared__ double2 bufL[1024];      // 16 KB
-    __shared__ double2 bufR[1024];      // 16 KB
+// One 256-thread workgroup per stereo block: LRMS decision, MDCT L/R and
+// overall scales, M/S lines, MLD threshold combination, SMR selection and the
+// band maxima (LDS atomic max on order-preserving keys).
+__global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
+                                                      PacMasterWork W, PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024], bufC[1024];    // 48 KB
+    __shared__ double2 leafv[2][64];
     __shared__ uint8_t lrms_s[PAC_NB];
-    const int lane = threadIdx.x;
+    __shared__ unsigned long long key[6][32];    // SMR 0/1, |line| 0/1, max|X| L/R
+    const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
+    if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
 
-    // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:96-102)
-    wave_spectrum_cplx([&](int i) { return rL(i); }, T, bufL, lane);
-    wave_spectrum_cplx([&](int i) { return rR(i); }, T, bufR, lane);
-    if (lane < PAC_NB) {
-        const int lo = T->lower[lane], m = T->nlines[lane];
-        auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
-            return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
-                                __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
-        };
+    // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:94-102)
+    grp_spectrum_cplx<256>([&](int i) { return rL(i); }, T, bufA, bufC, tid);
+    grp_spectrum_cplx<256>([&](int i) { return rR(i); }, T, bufB, bufC, tid);
+    auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
+        return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
+                            __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
+    };
+    if (tid < T->lr_nleaf) {
+        const int b = T->lr_leaf_band[tid], e0 = T->lr_leaf_e0[tid], n = T->lr_leaf_n[tid];
+        const int lo = T->lower[b];
         auto fd = [&](int e) {
-            double2 a = sq(bufL[lo + e]), b = sq(bufR[lo + e]);
-            return make_double2(__dsub_rn(a.x, b.x), __dsub_rn(a.y, b.y));
+            const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
+            return make_double2(__dsub_rn(a.x, c.x), __dsub_rn(a.y, c.y));
         };
         auto fs = [&](int e) {
-            double2 a = sq(bufL[lo + e]), b = sq(bufR[lo + e]);
-            return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
+            const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
+            return make_double2(__dadd_rn(a.x, c.x), __dadd_rn(a.y, c.y));
         };
-        double2 sd = np_csum<5>(fd, 0, 2 * m);
-        double2 ss = np_csum<5>(fs, 0, 2 * m);
-        int v = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
-        lrms_s[lane] = (uint8_t)v;
-        W.lrms[j * PAC_NB + lane] = (uint8_t)v;
+        leafv[0][tid] = np_csum_leaf(fd, e0, n);
+        leafv[1][tid] = np_csum_leaf(fs, e0, n);
     }
-    wave_sync();
+    __syncthreads();
+    if (tid < PAC_NB) {
+        int i0 = T->lr_first_leaf[tid], i1 = i0;
+        const int n = 2 * T->nlines[tid];
+        const double2 sd = np_csum_combine<5>(leafv[0], i0, n);
+        const double2 ss = np_csum_combine<5>(leafv[1], i1, n);
+        const int v = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
+        lrms_s[tid] = (uint8_t)v;
+        W.lrms[j * PAC_NB + tid] = (uint8_t)v;
+    }
+    __syncthreads();
 
-    // --- MDCT L and R, overall scale factors -------------------------------
-    double* XL = wave_mdct([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufL, lane);
-    double* XR = wave_mdct([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufR, lane);
-    double mxL = 0.0, mxR = 0.0;
+    // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
+    const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
+    const double* XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
+    double xl4[4], xr4[4];
+    double mL = 0.0, mR = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        mxL = fmax(mxL, fabs(XL[q * WAVE + lane]));
-        mxR = fmax(mxR, fabs(XR[q * WAVE + lane]));
+    for (int i = 0; i < 4; ++i) {
+        xl4[i] = XL[i * 256 + tid];
+        xr4[i] = XR[i * 256 + tid];
+        mL = fmax(mL, fabs(xl4[i]));
+        mR = fmax(mR, fabs(xr4[i]));
     }
-    const int oL = pac_scale_factor(wave_max(mxL), 5);
-    const int oR = pac_scale_factor(wave_max(mxR), 5);
+    atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
+    atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
+    __syncthreads();
+    const int oL = pac_scale_factor(__longlong_as_double((long long)key[4][0]), 5);
+    const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
     const double gL = (double)(1 << oL), gR = (double)(1 << oR);
     const double offL = 6.02 * oL, offR = 6.02 * oR;
-    if (lane == 0) { W.overall[j * 2] = (uint8_t)oL; W.overall[j * 2 + 1] = (uint8_t)oR; }
+    if (tid == 0) { W.overall[j * 2] = (uint8_t)oL; W.overall[j * 2 + 1] = (uint8_t)oR; }
 
-    // --- per-line SMR terms (psychoac.py:533-597) ---------------------------
-    double* dLR0 = reinterpret_cast<double*>(bufL + 512);   // second 8 KB of each buffer
-    double* dLR1 = reinterpret_cast<double*>(bufR + 512);
+    // --- per-line SMR terms (psychoac.py:533-597), selection (:662-682) ----
     const double* thr = W.thr + j * 6 * PAC_HALFN;
     double* lines = W.lines + j * 2 * PAC_HALFN;
-    double dM[16], dS[16];
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        int l = q * WAVE + lane;
-        double xl = __dmul_rn(XL[l], gL), xr = __dmul_rn(XR[l], gR);
-        double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
-        double splL = pac_spl(4. * (xl * xl)) - offL;
-        double splR = pac_spl(4. * (xr * xr)) - offR;
-        double splM = pac_spl(4. * (M * M)) - offL;
-        double splS = pac_spl(4. * (S * S)) - offR;
-        double bL = thr[0 * PAC_HALFN + l], bR = thr[1 * PAC_HALFN + l];
-        double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
-        double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
-        double mld = T->mld[l];
-        double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
-        double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
-        double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
-        double c = bM < mldM ? bM : mldM;
-        double thrS = bS > c ? bS : c;
-        dM[q] = splM - thrM;
-        dS[q] = splS - thrS;
-        int ms = lrms_s[T->band_of_line[l]];
-        lines[l] = ms ? M : xl;
-        lines[PAC_HALFN + l] = ms ? S : xr;
-        // stash L/R terms where the MDCT scratch was
-        XL[l] = splL - bL;      // XL/XR no longer needed once read above
-        XR[l] = splR - bR;
-    }
-    wave_sync();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        int l = q * WAVE + lane;
-        dLR0[l] = dM[q];
-        dLR1[l] = dS[q];
-    }
-    wave_sync();
-    if (lane < PAC_NB) {
-        const int lo = T->lower[lane], n = T->nlines[lane];
-        const int ms = lrms_s[lane];
-        double s0 = -INFINITY, s1 = -INFINITY, p0 = 0.0, p1 = 0.0;
-        for (int l = lo; l < lo + n; ++l) {
-            s0 = fmax(s0, ms ? dLR0[l] : XL[l]);
-            s1 = fmax(s1, ms ? dLR1[l] : XR[l]);
-            p0 = fmax(p0, fabs(lines[l]));
-            p1 = fmax(p1, fabs(lines[PAC_HALFN + l]));
+    for (int i = 0; i < 4; ++i) {
+        const int l = i * 256 + tid;
+        const double xl = __dmul_rn(xl4[i], gL), xr = __dmul_rn(xr4[i], gR);
+        const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
+        const double bL = thr[0 * PAC_HALFN + l], bR = thr[1 * PAC_HALFN + l];
+        const double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
+        const double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
+        const double mld = T->mld[l];
+        const double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
+        const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
+        const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
+        const double c = bM < mldM ? bM : mldM;
+        const double thrS = bS > c ? bS : c;
+        const int b = T->band_of_line[l];
+        const int ms = l < lend ? lrms_s[b] : 0;
+        double d0, d1;
+        if (ms) {
+            d0 = (pac_spl(4. * (M * M)) - offL) - thrM;
+            d1 = (pac_spl(4. * (S * S)) - offR) - thrS;
+        } else {
+            d0 = (pac_spl(4. * (xl * xl)) - offL) - bL;
+            d1 = (pac_spl(4. * (xr * xr)) - offR) - bR;
         }
-        if (n == 0) { s0 = -96.0; s1 = -96.0; }
-        W.smr[(j * 2 + 0) * PAC_NB + lane] = s0;
-        W.smr[(j * 2 + 1) * PAC_NB + lane] = s1;
-        W.bandpeak[(j * 2 + 0) * PAC_NB + lane] = p0;
-        W.bandpeak[(j * 2 + 1) * PAC_NB + lane] = p1;
+        const double v0 = ms ? M : xl, v1 = ms ? S : xr;
+        lines[l] = v0;
+        lines[PAC_HALFN + l] = v1;
+        if (l < lend) {
+            atomicMax(&key[0][b], pac_order_key(d0));
+            atomicMax(&key[1][b], pac_order_key(d1));
+            atomicMax(&key[2][b], (unsigned long long)__double_as_longlong(fabs(v0)));
+            atomicMax(&key[3][b], (unsigned long long)__double_as_longlong(fabs(v1)));
+        }
+    }
+    __syncthreads();
+    if (tid < PAC_NB) {
+        const bool has = T->nlines[tid] != 0;
+        W.smr[(j * 2 + 0) * PAC_NB + tid] = has ? pac_order_unkey(key[0][tid]) : -96.0;
+        W.smr[(j * 2 + 1) * PAC_NB + tid] = has ? pac_order_unkey(key[1][tid]) : -96.0;
+        W.bandpeak[(j * 2 + 0) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[2][tid]) : 0.0;
+        W.bandpeak[(j * 2 + 1) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[3][tid]) : 0.0;
     }
 }
 

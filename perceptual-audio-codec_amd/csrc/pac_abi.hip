@@ -171,6 +171,13 @@ static void build_tables(int fs, PacTables* t) {
         if (v > mx) mx = v;
     }
     for (int k = 0; k < PAC_HALFN; k++) t->mld[k] = t->mld[k] / mx;
+    for (int l = 0, ku = 0, kv = 0; l < PAC_HALFN; l++) {   // bark_line ascending in l
+        const double zl = t->bark_line[l];
+        while (ku < PAC_HALFN - 1 && zl - t->bark_bin[ku] > 0.5) ku++;
+        while (kv < PAC_HALFN - 1 && zl - t->bark_bin[kv] >= -0.5) kv++;
+        t->mask_ku[l] = (int16_t)ku;
+        t->mask_kv[l] = (int16_t)kv;
+    }
 }
 
 extern "C" int pac_band_layout(int32_t sample_rate, int32_t n_lines_out[25]) {

@@ -44,6 +44,12 @@ struct PacTables {
     int32_t lr_nleaf;
     int32_t lr_first_leaf[PAC_NB];
     int16_t lr_leaf_band[64], lr_leaf_e0[64], lr_leaf_n[64];
+    // masking-side bin bounds per MDCT line l (psychoac.py:111-116 slope choice):
+    // bin k carries a masker "below" l iff k < mask_ku[l]  (z_l - z_k >  1/2),
+    // "below or flat" iff k < mask_kv[l]                  (z_l - z_k >= -1/2);
+    // exact double comparisons, fl(z_l - z) is monotone in z.  With the rank
+    // of each bin among the maskers this gives the zone bounds U, V per line.
+    int16_t mask_ku[PAC_HALFN], mask_kv[PAC_HALFN];
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

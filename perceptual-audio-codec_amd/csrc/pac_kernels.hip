@@ -165,12 +165,12 @@ __device__ __forceinline__ double pac_order_unkey(unsigned long long k) {
 // into LDS; the MDCT runs first (lines kept in registers, band peaks taken),
 // then the Hann spectrum whose masker list the four waves share; the waves
 // claim the 16 masking rows of 64 lines dynamically.
-__global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
+__global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
     __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then per-wave beta rows
-    // exactly 32 KB of LDS (5 workgroups per CU): the small reduction scratch
-    // lives in whichever region is idle at that point
+    __shared__ int16_t rank[PAC_HALFN];   // 2 KB: masker rank of each bin (4 workgroups per CU)
+    // the small reduction scratch lives in whichever region is idle at that point
     int* cnt = reinterpret_cast<int*>(xs);         // free once the spectrum input is staged
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
     grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf,
                                reinterpret_cast<double2*>(xs), tid);
     PROF_MARK(4);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt, rank);
     PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     // Masking rows are claimed dynamically, most expensive first (the order
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(FRONT_NT, 5) void k_origin_front(PacSource src, con
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
-        const double thr = wave_masking_row(buf, nm, T, lane, r, xs + w * 512);
+        const double thr = wave_masking_row(buf, nm, T, lane, r, xs + w * 512, rank);
         switch (nr) {
             case 0: tv0 = thr; break;
             case 1: tv1 = thr; break;
@@ -503,9 +503,10 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
     wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
-    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane, reinterpret_cast<int*>(tmp));
+    int16_t* rank = reinterpret_cast<int16_t*>(tmp + 512);   // past the peak scratch
+    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane, reinterpret_cast<int*>(tmp), rank);
     double thr[16];
-    wave_masking(buf, nm, T, lane, thr, beta);
+    wave_masking(buf, nm, T, lane, thr, beta, rank);
 #pragma unroll
     for (int q = 0; q < 16; ++q) thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = thr[q];
     if (lane == 0) npeaks[blockIdx.x] = nm;

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
                                                          PacMasterWork W, PacMasterChunk ck) {
     __shared__ double2 buf[1024];
     __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // FFT / peak scratch, then beta rows
+    __shared__ int16_t rank[PAC_HALFN];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const BlockPcm rR(locate(src, gb, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta));
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta), rank);
     double* out = W.thr + (j * 6 + v) * PAC_HALFN;
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
-        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r, beta + w * 512);
+        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r, beta + w * 512, rank);
     }
 }
 

@@ -299,9 +299,11 @@ __device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<
 // NT threads.  scratch: LDS of 16 + 512 ints.  Returns the masker count.
 // Peaks are compacted first (ballots, bin order = the reference's summation
 // order) so that the SPL (a log10 each) is evaluated once per masker.
+// rank[k] (k < 1024) = #maskers with bin < k, for the zone bounds of the
+// masking sum (PacTables::mask_ku / mask_kv).
 template <int NT>
 __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                double drop, int tid, int* scratch) {
+                                                double drop, int tid, int* scratch, int16_t* rank) {
     constexpr int J = 1024 / NT;
     constexpr int NW = NT / WAVE;
     int* cnt = scratch;              // [J][NW] peak counts of the (j, wave) segments, in bin order
@@ -328,8 +330,11 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
     for (int i = 0; i < J * NW; ++i) { pre[i] = tot; tot += cnt[i]; }
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-        if ((bal[j] >> lane) & 1ull) kidx[pre[j * NW + w] + __popcll(bal[j] & below)] = j * NT + tid;
+    for (int j = 0; j < J; ++j) {
+        const int idx = pre[j * NW + w] + __popcll(bal[j] & below);
+        rank[j * NT + tid] = (int16_t)idx;
+        if ((bal[j] >> lane) & 1ull) kidx[idx] = j * NT + tid;
+    }
     grp_sync<NT>();
     tot = __builtin_amdgcn_readfirstlane(tot);
     constexpr int R = (PAC_MAXMASK + NT - 1) / NT;
@@ -369,8 +374,8 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
 }
 
 __device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                 double drop, int lane, int* scratch) {
-    return grp_find_maskers<WAVE>(buf, T, drop, lane, scratch);
+                                                 double drop, int lane, int* scratch, int16_t* rank) {
+    return grp_find_maskers<WAVE>(buf, T, drop, lane, scratch, rank);
 }
 
 // 2^(h + l) for a double-double exponent (|l| << ulp(h)): exp2(h) * (1 + l ln2)
@@ -422,7 +427,7 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // with the direct sum to ~1e-15 relative.  Lane owns line l = 64 r + lane.
 // beta: 512 doubles of LDS private to the calling wave.
 __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, const PacTables* __restrict__ T,
-                                                   int lane, int r, double* beta) {
+                                                   int lane, int r, double* beta, const int16_t* rank) {
     const double* mz = mk_z(const_cast<double2*>(buf));
     const double* mB = mk_B(const_cast<double2*>(buf));
     const double* mku = mk_ku(const_cast<double2*>(buf));
@@ -430,13 +435,10 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
     const int l = r * WAVE + lane;
     const double zl = T->bark_line[l];
     const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
-    // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending)
-    int lo = 0, hi = nm;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] > 0.5) lo = mid + 1; else hi = mid; }
-    const int U = lo;
-    hi = nm;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if (zl - mz[mid] >= -0.5) lo = mid + 1; else hi = mid; }
-    const int V = lo;
+    // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending),
+    // from the host-built bin bounds and the maskers' bin ranks
+    const int U = rank[T->mask_ku[l]];
+    const int V = rank[T->mask_kv[l]];
     // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
     //     gathered at each lane's V by a cross-lane shuffle (no LDS)
     const int vmin = wave_min_i(V);
@@ -563,7 +565,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
 
 // all 16 rows by one wave
 __device__ __forceinline__ void wave_masking(const double2* buf, int nm, const PacTables* __restrict__ T,
-                                             int lane, double thr[16], double* beta) {
+                                             int lane, double thr[16], double* beta, const int16_t* rank) {
 #pragma unroll 1
-    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r, beta);
+    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r, beta, rank);
 }

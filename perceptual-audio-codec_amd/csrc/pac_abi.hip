@@ -132,6 +132,17 @@ static void build_tables(int fs, PacTables* t) {
         t->peak_floor2 = m * m;
     }
     for (int i = 1; i < 64; i++) t->inv_int[i] = 1.0 / (double)i;
+    for (int d = 0; d < 64; d++) {
+        if (d > 40) { t->mom_eps[d] = INFINITY; continue; }     // PAC_MOM_DMAX
+        // ln remainder = eps + (d+1) ln eps - lgamma(d+2), increasing in eps
+        const long double lim = -57.0L * logl(2.0L), lg = lgammal((long double)d + 2.0L);
+        long double lo = 0.0L, hi = 64.0L;
+        for (int it = 0; it < 200; it++) {
+            const long double mid = 0.5L * (lo + hi);
+            if (mid + ((long double)d + 1.0L) * logl(mid) - lg <= lim) lo = mid; else hi = mid;
+        }
+        t->mom_eps[d] = (double)(lo * (1.0L - 1e-12L));          // conservative
+    }
     {   // numpy pairwise-sum leaves (loops_utils.h.src) of every band, in order
         int nl = 0;
         struct Rec {
@@ -528,6 +539,23 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G);
     HIPCHK(hipGetLastError());
     if (c->dbg & 16) report_phase_clocks(c, s, nprof);
+#ifdef PAC_ROWPROF
+    {
+        std::vector<unsigned long long> all(1024 * 16);
+        unsigned long long rp[16] = {0};
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(pac_rowprof), all.size() * 8));
+        for (int i = 0; i < 1024 * 16; i++) rp[i % 16] += all[i];
+        const double n = (double)(rp[0] ? rp[0] : 1);
+        fprintf(stderr, "ROWPROF rows %llu  cyc lower %.0f flat %.0f skip %.0f mom %.0f direct+rag %.0f | nm %.1f "
+                "momrows %.3f D %.2f mom_n %.1f rag %.1f flatlen %.1f lowlen %.1f m0 %.1f direct_n %.1f\n",
+                rp[0], rp[1] / n, rp[2] / n, rp[3] / n, rp[4] / n, rp[5] / n, rp[6] / n, rp[7] / n,
+                rp[8] / (double)(rp[7] ? rp[7] : 1), rp[9] / n, rp[10] / n, rp[11] / n, rp[12] / n, rp[13] / n,
+                rp[14] / n);
+        std::fill(all.begin(), all.end(), 0ull);
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pac_rowprof), all.data(), all.size() * 8));
+    }
+#endif
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_origin_alloc, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, T, W, G,
                        bit_budget(p), 16);

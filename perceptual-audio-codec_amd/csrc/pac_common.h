@@ -39,6 +39,9 @@ struct PacTables {
     // the square of the largest double m with 10*log10(m) <= -30 (host libm)
     double peak_floor2;
     double inv_int[64];           // 1/i (inv_int[0] unused)
+    // moment form of the masking sum (pac_wave.h): mom_eps[D] = largest eps with
+    // e^eps eps^(D+1)/(D+1)! <= 2^-57 (Taylor remainder), +inf past PAC_MOM_DMAX
+    double mom_eps[64];
     // leaves of numpy's pairwise complex sum over each band's FFT bins (the
     // LRMS decision, codec.py:96-102): band, first element, length in doubles
     int32_t lr_nleaf;

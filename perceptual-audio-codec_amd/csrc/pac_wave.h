@@ -426,6 +426,16 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // that only the ragged ends of each zone need a per-lane test.  Values agree
 // with the direct sum to ~1e-15 relative.  Lane owns line l = 64 r + lane.
 // beta: 512 doubles of LDS private to the calling wave.
+// diagnostic build (-DPAC_ROWPROF): cycle and size counters of the masking rows
+#ifdef PAC_ROWPROF
+__device__ unsigned long long pac_rowprof[1024 * 16];   // spread over 1024 lines: no hot address
+#define RP_T(v) long long v = (long long)__builtin_amdgcn_s_memtime()
+#define RP_ADD(i, x) do { if (lane == 0) atomicAdd(&pac_rowprof[(blockIdx.x & 1023) * 16 + (i)], (unsigned long long)(x)); } while (0)
+#else
+#define RP_T(v) do {} while (0)
+#define RP_ADD(i, x) do {} while (0)
+#endif
+
 __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, const PacTables* __restrict__ T,
                                                    int lane, int r, double* beta, const int16_t* rank) {
     const double* mz = mk_z(const_cast<double2*>(buf));
@@ -439,6 +449,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
     // from the host-built bin bounds and the maskers' bin ranks
     const int U = rank[T->mask_ku[l]];
     const int V = rank[T->mask_kv[l]];
+    RP_T(t0);
     // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
     //     gathered at each lane's V by a cross-lane shuffle (no LDS)
     const int vmin = wave_min_i(V);
@@ -468,20 +479,31 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
         dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
         lower = sv * pac_exp2_dd(h, lo2);
     }
+    RP_T(t1);
     // --- flat zone [U, V), ascending: ragged head, common middle, ragged tail
     double flat = 0.0;
     const int umin = wave_min_i(U), umax = wave_max_i(U), vmax = wave_max_i(V);
     const int fa = umax < vmax ? umax : vmax;
     const int fb = fa > vmin ? fa : vmin;
-    for (int m = umin; m < fa; ++m) {
-        const double e = mE[m];
-        flat += (m >= U && m < V) ? e : 0.0;
+    const int span = wave_max_i(V - U);           // longest flat zone of the row
+    if (span < vmax - umin) {                     // each lane walks its own zone
+        for (int i = 0; i < span; ++i) {
+            const int m = U + i;
+            const double e = mE[m < V ? m : 0];
+            flat += (m < V) ? e : 0.0;
+        }
+    } else {                                      // or the row's union of zones
+        for (int m = umin; m < fa; ++m) {
+            const double e = mE[m];
+            flat += (m >= U && m < V) ? e : 0.0;
+        }
+        for (int m = fa; m < fb; ++m) flat += mE[m];   // U <= umax <= m < vmin <= V on every lane
+        for (int m = fb; m < vmax; ++m) {
+            const double e = mE[m];
+            flat += (m >= U && m < V) ? e : 0.0;
+        }
     }
-    for (int m = fa; m < fb; ++m) flat += mE[m];   // U <= umax <= m < vmin <= V on every lane
-    for (int m = fb; m < vmax; ++m) {
-        const double e = mE[m];
-        flat += (m >= U && m < V) ? e : 0.0;
-    }
+    RP_T(t2);
     // --- upper side, ascending
     const double tiq = T->tiq[l];
     const double lb = wave_ext_f64<false>(tiq + flat + lower);   // I(l) >= lb on every lane
@@ -500,6 +522,7 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
         if (kb) { m0 = base + __builtin_ctzll(kb); break; }
     }
     m0 = __builtin_amdgcn_readfirstlane(m0 < umax ? m0 : umax);
+    RP_T(t3);
     // exponents relative to the row middle: 2^(beta_m + ku_m (z_l - z_mid))
     const double zm = 0.5 * (zr + T->bark_line[r * WAVE + WAVE - 1]);
     for (int m = m0 + lane; m < umax; m += WAVE)
@@ -526,29 +549,46 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
         const double adl = fmax(zm - zr, T->bark_line[r * WAVE + WAVE - 1] - zm);
         const double kc = 0.5 * (kmn + kmx);
         const double eps = (0.5 * (kmx - kmn) * adl) * PAC_LN2 * 1.0000001;
-        // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57 (uniform)
-        int D = 0;
-        double rem = pac_exp2(eps * 1.4426950408889634) * eps;  // e^eps eps^1/1!
-        while (rem > 0x1p-57 && D < PAC_MOM_DMAX + 1) { ++D; rem *= eps * T->inv_int[D + 1]; }
-        D = __builtin_amdgcn_readfirstlane(D);
+        // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57 (uniform): lane j tests
+        // eps against its bound; PAC_MOM_DMAX + 1 (no moment form) past the table
+        const unsigned long long ok = __ballot(eps <= T->mom_eps[lane]);
+        const int D = ok ? (int)__builtin_ctzll(ok) : PAC_MOM_DMAX + 1;
+#ifdef PAC_ROWPROF
+        RP_ADD(8, D);
+#endif
         if (D <= PAC_MOM_DMAX) {
             direct = false;
-            for (int m = m0 + lane; m < ua; m += WAVE) beta[m] = pac_exp2(beta[m]);   // own slots
             const double x = dl * PAC_LN2;
+            const double invl = T->inv_int[lane];      // 1/j in lane j
             double acc = 0.0, q = 1.0;
-            for (int d = 0; d <= D; ++d) {
-                double part = 0.0;
-                for (int m = m0 + lane; m < ua; m += WAVE) {
-                    const double p = beta[m];
-                    part += p;
-                    beta[m] = p * (mku[m] - kc);
+            if (ua - m0 <= 2 * WAVE) {                 // two maskers per lane, in registers
+                const int ma = m0 + lane, mb = ma + WAVE;
+                double p0 = 0.0, c0 = 0.0, p1 = 0.0, c1 = 0.0;
+                if (ma < ua) { p0 = pac_exp2(beta[ma]); c0 = mku[ma] - kc; }
+                if (mb < ua) { p1 = pac_exp2(beta[mb]); c1 = mku[mb] - kc; }
+                for (int d = 0; d <= D; ++d) {
+                    acc = __builtin_fma(wave_sum_f64(p0 + p1), q, acc);
+                    p0 *= c0;
+                    p1 *= c1;
+                    q = (q * x) * readlane_f64(invl, d + 1);
                 }
-                acc = __builtin_fma(wave_sum_f64(part), q, acc);
-                q = (q * x) * T->inv_int[d + 1];
+            } else {
+                for (int m = m0 + lane; m < ua; m += WAVE) beta[m] = pac_exp2(beta[m]);   // own slots
+                for (int d = 0; d <= D; ++d) {
+                    double part = 0.0;
+                    for (int m = m0 + lane; m < ua; m += WAVE) {
+                        const double p = beta[m];
+                        part += p;
+                        beta[m] = p * (mku[m] - kc);
+                    }
+                    acc = __builtin_fma(wave_sum_f64(part), q, acc);
+                    q = (q * x) * readlane_f64(invl, d + 1);
+                }
             }
             up = acc * pac_exp2(kc * dl);
         }
     }
+    RP_T(t4);
     if (direct) {
 #pragma unroll 2
         for (int m = m0; m < ua; ++m)               // m < umin <= U on every lane
@@ -560,6 +600,13 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
         up += (m < U) ? t : 0.0;
     }
     wave_sync();                                    // beta is rewritten by the next row
+    RP_T(t5);
+#ifdef PAC_ROWPROF
+    RP_ADD(0, 1); RP_ADD(1, t1 - t0); RP_ADD(2, t2 - t1); RP_ADD(3, t3 - t2); RP_ADD(4, t4 - t3);
+    RP_ADD(5, t5 - t4); RP_ADD(6, nm); RP_ADD(7, direct ? 0 : 1); RP_ADD(9, ua - m0);
+    RP_ADD(10, umax - ua); RP_ADD(11, vmax - umin); RP_ADD(12, nm - vmin); RP_ADD(13, m0);
+    RP_ADD(14, direct ? (ua - m0) : 0);
+#endif
     return pac_spl(((up + flat) + lower) + tiq);
 }
 

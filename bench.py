@@ -1,25 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark: stereo 1024-sample blocks encoded per second on MI355X.
 
-Workload (BASELINE.json configs[1], the config the metric is quoted on):
-synthetic 48 kHz stereo white noise, N(0,1)*0.25*32767 rounded/clipped to
-int16, 10^6 stereo blocks per GPU (1000 independent streams x 1000 blocks,
-999 hops + the Close() flush block each), origin profile ("M/S off":
-PerceptualAudioCodec_Origin's coder, the reference's own no-M/S encoder).
-The PCM is generated on the device (k_synth_white) so the timed region starts
-with the inputs resident in HBM; one step = one pac_encode_streams call over
-all 10^6 blocks (MDCT, masking threshold, bit allocation, quantization, bit
-packing into the .pac data sections, all in HBM).
+Workloads (BASELINE.json configs; --config picks one, default 2):
 
-    python bench.py [--gpus N --steps K --warmup W]
+  2  (default, the largest single-GPU config -- BASELINE.json's metric names
+     no config): synthetic 48 kHz stereo pink noise + 440/1250/5300 Hz tones,
+     10^7 stereo blocks per GPU as 10 000 independent streams x 1000 blocks
+     (999 hops + the Close() flush block each), master profile: full
+     psychoacoustics (6 masking thresholds), M/S decision, reservoir bit
+     allocation, Huffman (.wak) -- the reference's codec/ coder.
+  1  synthetic 48 kHz stereo white noise, 10^6 blocks per GPU (1000 x 1000),
+     origin profile ("M/S off": PerceptualAudioCodec_Origin's coder).
+  3  the reference's inputs/*.wav (stereo ones, shipped under
+     tests/fixtures/inputs/) x --copies, each copy an independent master +
+     Huffman stream (per-file reservoir exactly as the reference), whole
+     streams sharded over the ranks by pac_amd.shard.plan (LPT).
+
+The PCM is generated on (configs 1-2) or uploaded to (config 3) the device
+before the timed region, so the timed region starts with the inputs resident
+in HBM; one step = the pac_encode_streams call(s) over all of this rank's
+blocks (MDCT, masking thresholds, bit allocation, quantization, Huffman, bit
+packing into the .pac/.wak data sections, all in HBM).
+
+    python bench.py [--config C] [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Streams shard across ranks with no data-path collective (weak scaling); the
-only cross-rank traffic is the barrier and the max-over-ranks of the timer
-(gloo, CPU tensors).  Rank 0 prints one JSON line.
+Streams shard across ranks with no data-path collective (weak scaling for
+configs 1-2, strong for config 3); the only cross-rank traffic is the barrier
+and the max-over-ranks of the timer (gloo, CPU tensors).  Rank 0 prints one
+JSON line.
 """
 import argparse
 import ctypes as C
+import glob
 import json
 import os
 import sys
@@ -31,26 +44,30 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import pac_amd  # noqa: E402,F401
-from pac_amd import _lib  # noqa: E402
+from pac_amd import _lib, build as _build, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
+INPUTS = os.path.join(ROOT, "tests", "fixtures", "inputs")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, choices=[1, 2, 3], default=2,
+                    help="BASELINE.json configs[i]: 1 origin white noise 10^6, 2 master pink+tones 10^7 "
+                         "(default), 3 master real-audio file batch")
     ap.add_argument("--mode", choices=["encode", "decode"], default="encode",
                     help="encode = the metric (default); decode = pac_decode_streams of the same "
                          "workload's bitstream (encoded once, untimed)")
-    ap.add_argument("--profile", choices=["origin", "master"], default="origin",
-                    help="origin = BASELINE configs[1] (white noise, M/S off, the metric's config); "
-                         "master = configs[2] (pink noise + tones, M/S + Huffman)")
+    ap.add_argument("--profile", choices=["origin", "master"], default=None,
+                    help="legacy alias: origin = --config 1, master = --config 2")
     ap.add_argument("--streams", type=int, default=None,
-                    help="default 1000 (origin, 10^6 blocks) / 10000 (master, 10^7 blocks)")
+                    help="configs 1/2: streams per GPU (default 1000 / 10000)")
     ap.add_argument("--blocks-per-stream", type=int, default=1000)
+    ap.add_argument("--copies", type=int, default=1000, help="config 3: copies of every input file")
     ap.add_argument("--sample-rate", type=int, default=48000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (oracle on host cores)")
@@ -58,8 +75,12 @@ def parse():
                     help="host threads of the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
+    if a.profile is not None:
+        a.config = 1 if a.profile == "origin" else 2
+    a.master = a.config != 1
+    a.profile = "master" if a.master else "origin"
     if a.streams is None:
-        a.streams = 10000 if a.profile == "master" else 1000
+        a.streams = 10000 if a.config == 2 else 1000
     return a
 
 
@@ -80,21 +101,19 @@ class Dist:
         if self.td:
             self.td.barrier()
 
-    def max(self, v):
+    def _red(self, v, op):
         if not self.td:
             return v
         import torch
         t = torch.tensor([float(v)], dtype=torch.float64)
-        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        self.td.all_reduce(t, op=op)
         return float(t.item())
 
+    def max(self, v):
+        return self._red(v, self.td.ReduceOp.MAX if self.td else None)
+
     def sum(self, v):
-        if not self.td:
-            return v
-        import torch
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.td.all_reduce(t, op=self.td.ReduceOp.SUM)
-        return float(t.item())
+        return self._red(v, self.td.ReduceOp.SUM if self.td else None)
 
     def close(self):
         if self.td:
@@ -102,57 +121,71 @@ class Dist:
 
 
 # the reference's direct masking sum costs ~35 FP64
-# flops per (masker, line) pair, ~2 x 255 x 1024 pairs per stereo block for
-# the origin coder -> ~18 MFLOP per block.  Our kernel evaluates the same sum
-# in factored forms; "ref_alg_equiv_tflops" prices our rate at
-# the reference algorithm's flop count.
-REF_ALG_FLOP_PER_BLOCK = 18.0e6
-REF_ALG_FLOP_PER_BLOCK_MASTER = 48.0e6     # 6 thresholds x ~222 maskers x 1024 lines
+# flops per (masker, line) pair: origin ~2 x 255 x 1024 pairs per stereo block
+# (~18 MFLOP), master 6 x ~222 x 1024 (~48 MFLOP).  Our kernels evaluate the
+# same sums in factored forms; "ref_alg_equiv_tflops" prices our
+# rate at the reference algorithm's flop count.
+REF_ALG_FLOP_PER_BLOCK = {"origin": 18.0e6, "master": 48.0e6}
+
+# Algorithmic HBM bytes per stereo block of each kernel:
+# what the kernel must read and write, not what it happens to move.
+ALG_BYTES = {
+    "k_origin_front": 4096 + 2 * (25 * 8 * 2 + 1),   # int16 PCM in; SMR + band peaks + overall out
+    "k_master_thr": 4096 + 6 * 1024 * 8,             # int16 PCM in; 6 threshold rows out (calcBTHR x 6)
+    "k_master_front": 4096 + 6 * 1024 * 8 + 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2,
+    "k_master_tail": 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2 * (25 * 2 + 1 + 4 + 8),
+    "k_master_pack": 2 * 1024 * 8 + 2 * 25 * 2 + 25 + 2 + 2 * 300,
+}
 
 
-def measured_profile():
-    """Per-block HBM bytes and FP64 work of k_origin_front from the newest
-    committed rocprofv3 PMC summary (profiles/*_origin_pmc.json, made by
-    profiles/run_profile.sh + profiles/summarize_pmc.py on this kernel build)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_origin_pmc.json")))
+def measured_profile(kind, kernel):
+    """Per-block HBM bytes and FP64 work of `kernel` from the newest committed
+    rocprofv3 PMC summary profiles/r*_<kind>_pmc.json (profiles/run_profile.sh
+    + profiles/summarize_pmc.py), used only if its recorded source hash equals
+    this build's: counters from another build are reported as stale, never
+    combined with this build's times."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_pmc.json" % kind)))
     if not files:
-        return None
+        return None, "no profiles/r*_%s_pmc.json" % kind
     with open(files[-1]) as f:
         d = json.load(f)
-    if "k_origin_front" not in d:
-        return None
-    d["_file"] = os.path.relpath(files[-1], ROOT)
-    return d
+    rel = os.path.relpath(files[-1], ROOT)
+    if d.get("src_hash") != _build.source_hash():
+        return None, "%s is stale (src_hash %s, this build %s)" % (rel, d.get("src_hash"), _build.source_hash())
+    k = d.get("kernels", {}).get(kernel)
+    if not k or not k.get("derived"):
+        return None, "%s has no counters for %s" % (rel, kernel)
+    out = dict(k["derived"])
+    out["_file"] = rel
+    return out, rel
 
 
-def cpu_baseline(ctx, dev_pcm, frames_per_stream, n_streams, fs, seconds, profile, threads):
+def cpu_baseline(ctx, samples, fs, seconds, profile, threads):
     """The CPU oracle (oracle/pac_oracle.c) on a bounded sample of the same
     workload, one host thread per stream (ctypes releases the GIL; the C
-    oracle keeps no global state): thread t encodes growing prefixes of stream
-    t, copied back from HBM, until `seconds` have passed."""
+    oracle keeps no global state): thread t encodes growing prefixes of its
+    stream (int16 frames copied back from HBM) until `seconds` have passed.
+    Returns the baseline and each thread's last (longest) data section."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as P
     from concurrent.futures import ThreadPoolExecutor
     P.lib()
-    threads = max(1, min(threads, n_streams))
-    hops = min(frames_per_stream // 1024, 4096)
-    pcms = []
-    for t in range(threads):
-        pcm = np.empty((hops * 1024, 2), dtype=np.int16)
-        ctx.to_host(pcm, dev_pcm + t * frames_per_stream * 4)
-        pcms.append(pcm)
+    threads = max(1, min(threads, len(samples)))
     prof = P.MASTER if profile == "master" else P.ORIGIN
     t0 = time.perf_counter()
 
     def work(t):
         o = P.Oracle(fs, huffman=(prof == P.MASTER))
+        pcm = samples[t]
+        full = (pcm.shape[0] + 1023) // 1024 + 1
         done, chunk, last = 0, 16, b""
         while time.perf_counter() - t0 < seconds and done < 200000:
-            n = min(chunk, hops - 1)
-            last = o.encode_data(prof, pcms[t][: n * 1024], max_blocks=n)
+            n = min(chunk, full)
+            last = o.encode_data(prof, pcm, max_blocks=n)
             done += n
-            chunk = min(chunk * 2, hops - 1)
+            if n == full:
+                break
+            chunk = min(chunk * 2, full)
         return done, last
 
     with ThreadPoolExecutor(threads) as ex:
@@ -161,8 +194,8 @@ def cpu_baseline(ctx, dev_pcm, frames_per_stream, n_streams, fs, seconds, profil
     done = sum(r[0] for r in res)
     base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
-                      "fixtures), %s profile, %d host threads (one stream each), %d stereo "
-                      "blocks of the same synthetic streams in %.1f s" % (profile, threads, done, el)}
+                      "fixtures), %s profile, %d host threads (one stream each, growing prefixes), "
+                      "%d stereo blocks of the same streams in %.1f s" % (profile, threads, done, el)}
     return base, [r[1] for r in res]
 
 
@@ -176,16 +209,16 @@ def channel_blocks(b):
     return out
 
 
-def parity_check(ctx, out_dev, so, oracle_prefixes):
-    """The oracle's bytes for the first blocks of streams 0..T-1 (from the CPU
-    baseline run) against the GPU's bytes for the same streams: the number of
-    channel-blocks compared and how many differ (flip rate)."""
+def parity_check(ctx, out_dev, starts, oracle_prefixes):
+    """The oracle's bytes for the first blocks of the sampled streams against
+    the GPU's bytes for the same streams: channel-blocks compared and how many
+    differ (flip rate)."""
     checked = bad = 0
-    for t, ref in enumerate(oracle_prefixes):
+    for st, ref in zip(starts, oracle_prefixes):
         if not ref:
             continue
         got = np.empty(len(ref), dtype=np.uint8)
-        ctx.to_host(got, out_dev + int(so[t]))
+        ctx.to_host(got, out_dev + int(st))
         a, b = channel_blocks(ref), channel_blocks(got.tobytes())
         checked += len(a)
         bad += sum(1 for x, y in zip(a, b) if x != y) + max(0, len(a) - len(b))
@@ -193,15 +226,83 @@ def parity_check(ctx, out_dev, so, oracle_prefixes):
             "against": "oracle/pac_oracle.c on the CPU-baseline sample"}
 
 
-def bench_decode(a, dist, ctx, p, encode_step, out_dev, ns, blocks, master):
+class Job:
+    """One pac_encode_streams call: streams sharing (sample rate, channels)
+    with their PCM resident in HBM."""
+
+    def __init__(self, ctx, p, fo, pcm_dev):
+        self.ctx, self.p, self.fo, self.pcm_dev = ctx, p, fo, pcm_dev
+        self.ns = len(fo) - 1
+        self.blocks = int(sum(shard.blocks_of(fo[i + 1] - fo[i]) for i in range(self.ns)))
+        self.cap = int(ctx.L.pac_encode_bound(C.byref(p), self.ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
+        self.out_dev = ctx.alloc(self.cap)
+        self.so = None
+
+    def run(self):
+        _, self.so = self.ctx.encode_streams(self.p, self.pcm_dev, self.fo, out=self.out_dev,
+                                             out_capacity=self.cap, pcm_is_device=True, out_is_device=True)
+        return self.ctx.last_timing()
+
+    def free(self):
+        self.ctx.free(self.out_dev)
+        self.ctx.free(self.pcm_dev)
+
+
+def synthetic_job(a, ctx, rank):
+    fs = a.sample_rate
+    fps = (a.blocks_per_stream - 1) * 1024
+    n_frames = a.streams * fps
+    fo = np.arange(a.streams + 1, dtype=np.int64) * fps
+    p = _lib.params(fs, 2, 1 if a.master else 0)
+    pcm_dev = ctx.alloc(n_frames * 2 * 2)
+    if a.master:
+        ctx.synth_pink_tones(pcm_dev, n_frames, fs, seed=1234 + 7919 * rank)
+    else:
+        ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * rank)
+    return [Job(ctx, p, fo, pcm_dev)]
+
+
+def file_jobs(a, ctx, rank, world):
+    """config 3: stereo inputs x copies, this rank's LPT shard, one job per
+    sample rate.  Returns (jobs, description)."""
+    from pac_amd.pcmfile import read_for_encode
+    paths = sorted(glob.glob(os.path.join(INPUTS, "*.wav")))
+    reads = [(os.path.basename(pth), *read_for_encode(pth)) for pth in paths]
+    stereo = [(n, cp, fr) for n, cp, fr in reads if cp.nChannels == 2]
+    streams = [(i, c) for i in range(len(stereo)) for c in range(a.copies)]
+    counts = [shard.blocks_of(stereo[i][2].shape[0]) for i, _ in streams]
+    mine = shard.plan(counts, world)[rank]
+    by_fs = {}
+    for k in mine:
+        i, _ = streams[k]
+        by_fs.setdefault(stereo[i][1].sampleRate, []).append(i)
+    jobs = []
+    for fs, files in sorted(by_fs.items()):
+        lens = np.array([stereo[i][2].shape[0] for i in files], dtype=np.int64)
+        fo = np.zeros(len(files) + 1, dtype=np.int64)
+        fo[1:] = np.cumsum(lens)
+        pcm_dev = ctx.alloc(max(int(fo[-1]) * 4, 4))
+        # upload file by file (no host copy of the whole tiled batch)
+        for j, i in enumerate(files):
+            ctx.to_device(pcm_dev + int(fo[j]) * 4, stereo[i][2])
+        jobs.append(Job(ctx, _lib.params(fs, 2, 1), fo, pcm_dev))
+    desc = {"inputs": ["%s (%d Hz, %d frames)" % (n, cp.sampleRate, fr.shape[0]) for n, cp, fr in stereo],
+            "skipped_mono": [n for n, cp, _ in reads if cp.nChannels != 2],
+            "copies": a.copies, "streams_total": len(streams), "streams_this_rank": len(mine)}
+    return jobs, desc, stereo
+
+
+def bench_decode(a, dist, ctx, job):
     """Decoder throughput: the workload's bitstream (encoded once on the GPU,
     untimed) decoded by pac_decode_streams with input and output in HBM."""
-    _, so = encode_step()
-    frames = blocks * 1024
+    job.run()
+    so = job.so
+    frames = job.blocks * 1024
     pcm_out = ctx.alloc(frames * 2 * 2)
+    p = job.p
 
     def step():
-        return ctx.decode_streams(p, out_dev, so, data_is_device=True, out=pcm_out,
+        return ctx.decode_streams(p, job.out_dev, so, data_is_device=True, out=pcm_out,
                                   out_capacity_frames=frames, out_is_device=True)
 
     for _ in range(a.warmup):
@@ -218,10 +319,8 @@ def bench_decode(a, dist, ctx, p, encode_step, out_dev, ns, blocks, master):
     ctx.sync()
     dist.barrier()
     el_max = dist.max(time.perf_counter() - t0)
-    total_blocks = dist.sum(blocks)
+    total_blocks = dist.sum(job.blocks)
     in_bytes = int(so[-1])
-    # algorithmic bytes per launch of the decode path: the bitstream read once
-    # + int16 PCM written once
     dec_s = (float(np.mean(parse_ms)) + float(np.mean(synth_ms))) / 1e3
     alg = in_bytes + frames * 4
     res = {
@@ -236,10 +335,10 @@ def bench_decode(a, dist, ctx, p, encode_step, out_dev, ns, blocks, master):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic, encoded on the GPU from %s" % ("pink noise + tones" if master else "white noise"),
-        "config": {"workload": "decode of the %s workload's bitstream (%d stereo blocks per GPU)"
-                               % ("configs[2]" if master else "configs[1]", blocks),
-                   "profile": a.profile, "streams_per_gpu": ns, "blocks_per_stream": a.blocks_per_stream,
+        "data": "synthetic, encoded on the GPU from %s" % ("pink noise + tones" if a.master else "white noise"),
+        "config": {"workload": "decode of the configs[%d] workload's bitstream (%d stereo blocks per GPU)"
+                               % (a.config, job.blocks),
+                   "profile": a.profile, "streams_per_gpu": job.ns, "blocks_per_stream": a.blocks_per_stream,
                    "global_blocks": int(total_blocks),
                    "parallelism": "streams sharded, %d rank(s)" % dist.world},
         "roofline": {"bound": "hbm", "kernel": "k_dec_parse + k_dec_synth", "achieved": alg / dec_s / 1e9,
@@ -247,16 +346,16 @@ def bench_decode(a, dist, ctx, p, encode_step, out_dev, ns, blocks, master):
                      "traffic": None},
         "kernels_ms": {"parse": float(np.mean(parse_ms)), "synth": float(np.mean(synth_ms))},
         "bitstream_bytes_per_gpu": in_bytes,
+        "src_hash": _build.source_hash(),
     }
     if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
-        res["cpu_baseline"], res["parity"] = cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master)
+        res["cpu_baseline"], res["parity"] = cpu_decode(ctx, p, job.out_dev, so, pcm_out, fo, a)
     ctx.free(pcm_out)
     if dist.rank == 0:
         print(json.dumps(res))
-    dist.close()
 
 
-def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master):
+def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a):
     """The oracle's decoder on the first streams' bytes (one host thread per
     stream, bounded), and its frames against the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -272,11 +371,11 @@ def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master):
     t0 = time.perf_counter()
 
     def work(t):
-        o = P.Oracle(a.sample_rate, huffman=master)
+        o = P.Oracle(p.sample_rate, huffman=a.master)
         n = 0
         ref = None
         while time.perf_counter() - t0 < a.cpu_seconds or ref is None:
-            ref = o.decode_data(P.MASTER if master else P.ORIGIN, secs[t], 2)
+            ref = o.decode_data(P.MASTER if a.master else P.ORIGIN, secs[t], 2)
             n += ref.shape[0] // 1024
         return n, ref
 
@@ -297,88 +396,93 @@ def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a, master):
                   "against": "oracle/pac_oracle.c decoder on the CPU-baseline sample"}
 
 
+PHASES = {  # pac_timing field -> kernel, per profile (include/pac_gpu.h)
+    "origin": [("front_ms", "k_origin_front"), ("alloc_ms", "k_origin_alloc"), ("scan_ms", "k_scan"),
+               ("pack_ms", "k_origin_pack")],
+    "master": [("thr_ms", "k_master_thr"), ("front_ms", "k_master_front"), ("alloc_ms", "k_master_tail"),
+               ("pack_ms", "k_master_pack"), ("scan_ms", "k_copy_streams")],
+}
+
+
 def main():
     a = parse()
     dist = Dist()
-    master = a.profile == "master"
-    ctx = _lib.Context(dist.local, huffman=master)
-    fs = a.sample_rate
-    hops = a.blocks_per_stream - 1
-    fps = hops * 1024
-    ns = a.streams
-    n_frames = ns * fps
-    fo = np.arange(ns + 1, dtype=np.int64) * fps
-    p = _lib.params(fs, 2, 1 if master else 0)
-    blocks = ns * a.blocks_per_stream
-    pcm_dev = ctx.alloc(n_frames * 2 * 2)
-    if master:
-        ctx.synth_pink_tones(pcm_dev, n_frames, fs, seed=1234 + 7919 * dist.rank)
+    ctx = _lib.Context(dist.local, huffman=a.master)
+    desc, stereo = None, None
+    if a.config == 3:
+        jobs, desc, stereo = file_jobs(a, ctx, dist.rank, dist.world)
     else:
-        ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * dist.rank)
-    cap = int(ctx.L.pac_encode_bound(C.byref(p), ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
-    out_dev = ctx.alloc(cap)
+        jobs = synthetic_job(a, ctx, dist.rank)
     ctx.set_timing(True)
+    if a.mode == "decode":
+        bench_decode(a, dist, ctx, jobs[0])
+        for j in jobs:
+            j.free()
+        dist.close()
+        return
 
     def step():
-        return ctx.encode_streams(p, pcm_dev, fo, out=out_dev, out_capacity=cap,
-                                  pcm_is_device=True, out_is_device=True)
-
-    if a.mode == "decode":
-        return bench_decode(a, dist, ctx, p, step, out_dev, ns, blocks, master)
+        ms = {f: 0.0 for f, _ in PHASES[a.profile]}
+        for j in jobs:
+            t = j.run()
+            for f in ms:
+                ms[f] += getattr(t, f)
+        return ms
 
     for _ in range(a.warmup):
         step()
-    fronts, alloc_ms, pack_ms, totals = [], [], [], []
+    per = []
     dist.barrier()
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        _, so = step()
-        t = ctx.last_timing()
-        fronts.append(t.front_ms)
-        alloc_ms.append(t.alloc_ms)
-        pack_ms.append(t.pack_ms)
-        totals.append(t.total_ms)
+        per.append(step())
     ctx.sync()
     dist.barrier()
     el = time.perf_counter() - t0
     el_max = dist.max(el)
-    out_bytes = int(so[-1])
+    blocks = sum(j.blocks for j in jobs)
+    out_bytes = sum(int(j.so[-1]) for j in jobs if j.so is not None)
     total_blocks = dist.sum(blocks)
     value = total_blocks / (el_max / a.steps)
 
-    # roofline of the dominant kernel.  origin: k_origin_front, algorithmic
-    # bytes per launch = int16 PCM read (4096 B per stereo block) + SMR/peak/
-    # scale outputs (2 x (25*8 + 25*8 + 1) B per stereo block).  master: the
-    # front time covers k_master_thr + k_master_front; k_master_thr reads the
-    # PCM (4096 B) and writes the 6 thresholds (6 x 1024 x 8 B) per block.
-    front_s = float(np.mean(fronts)) / 1e3
-    kern = "k_master_thr" if master else "k_origin_front"
-    per_block = 4096 + (6 * 1024 * 8 if master else 2 * (25 * 8 * 2 + 1))
-    alg_bytes = blocks * per_block
-    achieved = alg_bytes / front_s / 1e9
-    prof = None if master else measured_profile()
+    kern_ms = {k: float(np.mean([p[f] for p in per])) for f, k in PHASES[a.profile]}
+    dom = max(kern_ms, key=kern_ms.get)
+    dom_s = kern_ms[dom] / 1e3
+    alg_bytes = blocks * ALG_BYTES.get(dom, 4096)
+    achieved = alg_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
+    prof, prof_note = measured_profile(a.profile, dom)
     traffic = None
-    ref_flop = REF_ALG_FLOP_PER_BLOCK_MASTER if master else REF_ALG_FLOP_PER_BLOCK
+    ref_flop = REF_ALG_FLOP_PER_BLOCK[a.profile]
+    step_s = sum(kern_ms.values()) / 1e3
     fp64 = {"ref_alg_flop_per_block": ref_flop,
-            "ref_alg_equiv_tflops": ref_flop * blocks / front_s / 1e12,
-            "peak_tflops": FP64_PEAK_TFLOPS}
+            "ref_alg_equiv_tflops": ref_flop * blocks / step_s / 1e12 if step_s else None,
+            "peak_tflops": FP64_PEAK_TFLOPS, "profile": prof_note}
     if prof:
-        f = prof["k_origin_front"]
-        traffic = (f["hbm_read_bytes_per_block"] + f["hbm_write_bytes_per_block"]) * blocks
-        fp64.update({"executed_flop_per_block": f["fp64_flop_per_block"],
-                     "executed_tflops": f["fp64_flop_per_block"] * blocks / front_s / 1e12,
-                     "executed_frac": f["fp64_flop_per_block"] * blocks / front_s / 1e12 / FP64_PEAK_TFLOPS,
-                     "valu_issue_util": f["valu_issue_util"], "source": prof["_file"]})
-    if master:
+        if "hbm_read_bytes_per_block" in prof:
+            traffic = (prof["hbm_read_bytes_per_block"] + prof["hbm_write_bytes_per_block"]) * blocks
+        if "fp64_flop_per_block" in prof:
+            tf = prof["fp64_flop_per_block"] * blocks / dom_s / 1e12
+            fp64.update({"kernel": dom, "executed_flop_per_block": prof["fp64_flop_per_block"],
+                         "executed_tflops": tf, "executed_frac": tf / FP64_PEAK_TFLOPS})
+        for k in ("valu_issue_util", "fp64_share_of_valu", "lds_bank_conflict_frac"):
+            if k in prof:
+                fp64[k] = prof[k]
+    if a.config == 2:
         data = "synthetic (device-generated pink noise (Voss, counter hash) + 440/1250/5300 Hz tones)"
-        workload = ("BASELINE configs[2]: synthetic 48 kHz stereo pink noise + tones, %d stereo "
-                    "blocks per GPU, N=1024 MDCT, full psychoacoustics + M/S + bit allocation + "
-                    "Huffman (master profile)" % blocks)
-    else:
+        workload = ("BASELINE configs[2]: synthetic 48 kHz stereo pink noise + tones, %d stereo blocks per GPU "
+                    "(%d streams x %d blocks), N=1024 MDCT, full psychoacoustics + M/S + bit allocation + "
+                    "Huffman (master profile)" % (blocks, a.streams, a.blocks_per_stream))
+    elif a.config == 1:
         data = "synthetic (device-generated white noise, counter-hash Box-Muller)"
-        workload = ("BASELINE configs[1]: synthetic 48 kHz stereo white noise, 10^6 stereo blocks "
-                    "per GPU, N=1024 MDCT, M/S off (origin profile)")
+        workload = ("BASELINE configs[1]: synthetic 48 kHz stereo white noise, %d stereo blocks per GPU "
+                    "(%d streams x %d blocks), N=1024 MDCT, M/S off (origin profile)"
+                    % (blocks, a.streams, a.blocks_per_stream))
+    else:
+        data = "real audio: the reference's inputs/*.wav (stereo), tiled as independent streams"
+        workload = ("BASELINE configs[3]: %d stereo inputs/*.wav x %d copies, each copy an independent "
+                    "master+Huffman stream, LPT-sharded over %d rank(s); %d stereo blocks on rank 0"
+                    % (len(stereo), a.copies, dist.world, blocks))
     res = {
         "metric": "stereo 1024-sample blocks encoded/s",
         "value": value,
@@ -388,32 +492,45 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": el_max / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.config == 3 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": data,
-        "config": {"workload": workload,
-                   "profile": a.profile, "sample_rate": fs, "streams_per_gpu": ns,
-                   "blocks_per_stream": a.blocks_per_stream,
-                   "global_blocks": int(total_blocks), "parallelism": "streams sharded, %d rank(s)"
+        "config": {"workload": workload, "profile": a.profile, "global_blocks": int(total_blocks),
+                   "blocks_per_gpu": blocks, "parallelism": "streams sharded, %d rank(s), no collective"
                    % dist.world},
-        "roofline": {"bound": "hbm", "kernel": kern, "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "traffic_source": prof["_file"] if prof else None,
-                     "note": "%s is FP64-VALU bound (masking sum), not HBM bound: "
-                             "see 'fp64' and DESIGN.md section 4" % kern},
+                     "traffic": traffic, "alg_bytes_per_block": ALG_BYTES.get(dom, 4096),
+                     "traffic_source": prof_note,
+                     "note": "%s is FP64-VALU bound (masking sum), not HBM bound: see 'fp64' and "
+                             "DESIGN.md section 4" % dom},
         "fp64": fp64,
-        "kernels_ms": {"front": float(np.mean(fronts)), "alloc": float(np.mean(alloc_ms)),
-                       "pack": float(np.mean(pack_ms)), "step_device": float(np.mean(totals))},
+        "kernels_ms": kern_ms,
         "out_bytes_per_gpu": out_bytes,
+        "src_hash": _build.source_hash(),
     }
+    if desc:
+        res["config"]["files"] = desc
+    else:
+        res["config"].update({"sample_rate": a.sample_rate, "streams_per_gpu": a.streams,
+                              "blocks_per_stream": a.blocks_per_stream})
     if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
-        res["cpu_baseline"], prefixes = cpu_baseline(ctx, pcm_dev, fps, ns, fs, a.cpu_seconds, a.profile,
-                                                     a.cpu_threads)
-        res["parity"] = parity_check(ctx, out_dev, so, prefixes)
-    ctx.free(out_dev)
-    ctx.free(pcm_dev)
+        # the CPU sample: the first streams of the (first) job, copied back from HBM
+        j = jobs[0]
+        nt = max(1, min(a.cpu_threads, j.ns))
+        samples, starts = [], []
+        for t in range(nt):
+            n = int(j.fo[t + 1] - j.fo[t])
+            n = min(n, 4096 * 1024)
+            pcm = np.empty((n, 2), dtype=np.int16)
+            ctx.to_host(pcm, j.pcm_dev + int(j.fo[t]) * 4)
+            samples.append(pcm)
+            starts.append(int(j.so[t]))
+        res["cpu_baseline"], prefixes = cpu_baseline(ctx, samples, j.p.sample_rate, a.cpu_seconds, a.profile, nt)
+        res["parity"] = parity_check(ctx, j.out_dev, starts, prefixes)
+    for j in jobs:
+        j.free()
     if dist.rank == 0:
         print(json.dumps(res))
     dist.close()

@@ -57,15 +57,22 @@ typedef struct {
     int64_t bit_deposit;
 } pac_stream_state;
 
-/* Per-kernel device time of the last encode call (HIP events), ms. */
+/* Per-kernel device time of the last encode call (HIP events recorded on the
+ * context's stream around each launch, read after the call), ms.
+ *   origin: front = k_origin_front, alloc = k_origin_alloc, scan = k_scan_*,
+ *           pack = k_origin_pack, thr = 0
+ *   master: thr = k_master_thr, front = k_master_front, alloc = k_master_tail,
+ *           pack = k_master_pack, scan = k_copy_streams (summed over chunks) */
 typedef struct {
-    float front_ms;     /* masking-threshold + MDCT front end (dominant) */
-    float alloc_ms;     /* bit allocation                                */
-    float scan_ms;      /* byte-offset scan                              */
-    float pack_ms;      /* quantize + bit packing                        */
-    float total_ms;     /* first to last event                           */
+    float front_ms;
+    float alloc_ms;
+    float scan_ms;
+    float pack_ms;
+    float total_ms;     /* sum of the phases (master) / first to last event (origin) */
     int64_t n_channel_blocks;
     int64_t out_bytes;
+    float thr_ms;
+    float reserved_ms;
 } pac_timing;
 
 /* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */

@@ -25,6 +25,17 @@ def cmd():
             "-fPIC", "-shared", "-Wno-unused-value", "-Wno-unused-result", "-o", LIB, SRC]
 
 
+def source_hash():
+    """sha256 (16 hex digits) of the kernel + C-ABI sources: profiles record
+    it so that bench.py can refuse counters taken on a different build"""
+    import hashlib
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def up_to_date():
     if not os.path.exists(LIB):
         return False

@@ -259,7 +259,16 @@ struct pac_ctx {
     // timing
     bool timing = false;
     hipEvent_t ev[5] = {};
+    std::vector<hipEvent_t> evpool;         // master: events of every chunk, read after the call
     pac_timing last = {};
+    hipEvent_t pool_event(size_t i) {
+        while (evpool.size() <= i) {
+            hipEvent_t e = nullptr;
+            hipEventCreate(&e);
+            evpool.push_back(e);
+        }
+        return evpool[i];
+    }
 };
 
 extern "C" int pac_ctx_create(int device, pac_ctx** out) {
@@ -300,6 +309,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
     c->stream_off.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
     for (auto& e : c->ev) hipEventDestroy(e);
+    for (auto& e : c->evpool) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -568,21 +578,21 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                        c->off.p);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
-    int64_t total = 0;
-    HIPCHK(hipMemcpyAsync(&total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (total > out_cap) return set_err(PAC_E_CAPACITY, "output needs %lld bytes, capacity %lld",
-                                        (long long)total, (long long)out_cap);
-    hipLaunchKernelGGL(k_origin_pack, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G, c->off.p, out_dev);
+    // no host round trip inside the pipeline: the pack kernel skips any
+    // channel-block that would end past out_cap, the caller checks the total
+    // (c->grand_total) after the call and reports PAC_E_CAPACITY
+    hipLaunchKernelGGL(k_origin_pack, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G, c->off.p, out_dev,
+                       out_cap);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[4], s));
-    *out_total = total;
+    HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     *off_dev = c->off.p;
     return PAC_OK;
 }
 
 static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     if (!c->timing) return;
+    c->last.thr_ms = 0.f;
     hipEventSynchronize(c->ev[4]);
     hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
     hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
@@ -622,7 +632,17 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         return rc;
     hipStream_t s = c->stream;
     const double budget = bit_budget(p);
-    float t_front = 0, t_alloc = 0, t_copy = 0, t_pack = 0;
+    // timing: events recorded around every launch, read once after the call
+    // (no host round trip inside the pipeline); marks[i] = (event, phase)
+    std::vector<std::pair<size_t, int>> marks;
+    size_t nev = 0;
+    auto mark = [&](int phase) -> int {
+        if (!c->timing) return PAC_OK;
+        const hipEvent_t e = c->pool_event(nev);
+        marks.emplace_back(nev++, phase);
+        HIPCHK(hipEventRecord(e, s));
+        return PAC_OK;
+    };
     std::vector<int64_t> so(n_streams + 1, 0), src_off(n_streams), cursor(n_streams), dst(n_streams),
         size(n_streams);
     int64_t total = 0;
@@ -660,27 +680,20 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         for (int64_t t0 = 0; t0 < gmax; t0 += S) {
             const PacMasterChunk ck{g0, n_s, t0, S};
             const int64_t B = (int64_t)n_s * S;
-            if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+            if ((rc = mark(-1))) return rc;
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, ck);
+            if ((rc = mark(0))) return rc;
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s, src, T, W, ck);
             HIPCHK(hipGetLastError());
-            if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
+            if ((rc = mark(1))) return rc;
             hipLaunchKernelGGL(k_master_tail, dim3((unsigned)n_s), dim3(64), 0, s, T, c->huff, W, c->blk_off.p, ck,
                                c->st_extra.p, c->st_deposit.p, c->st_cursor.p, c->off.p, budget);
             HIPCHK(hipGetLastError());
-            if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
+            if ((rc = mark(2))) return rc;
             hipLaunchKernelGGL(k_master_pack, dim3((unsigned)(2 * B)), dim3(64), 0, s, T, c->huff, W,
                                c->blk_off.p, ck, c->off.p, c->m_stage.p);
             HIPCHK(hipGetLastError());
-            if (c->timing) {
-                HIPCHK(hipEventRecord(c->ev[4], s));
-                HIPCHK(hipEventSynchronize(c->ev[4]));
-                float a, b2, d;
-                hipEventElapsedTime(&a, c->ev[1], c->ev[2]);
-                hipEventElapsedTime(&b2, c->ev[2], c->ev[3]);
-                hipEventElapsedTime(&d, c->ev[3], c->ev[4]);
-                t_front += a; t_alloc += b2; t_pack += d;
-            }
+            if ((rc = mark(3))) return rc;
         }
         // --- final offsets of the group's streams, then the copy
         HIPCHK(hipMemcpyAsync(cursor.data() + g0, c->st_cursor.p + g0, n_s * sizeof(int64_t),
@@ -699,28 +712,30 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                               hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->m_dst_off.p + g0, dst.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->m_size.p + g0, size.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
+        if ((rc = mark(-1))) return rc;
         hipLaunchKernelGGL(k_copy_streams, dim3((unsigned)n_s), dim3(256), 0, s, c->m_stage.p, c->m_src_off.p + g0,
                            c->m_dst_off.p + g0, c->m_size.p + g0, out_dev);
         HIPCHK(hipGetLastError());
-        if (c->timing) {
-            HIPCHK(hipEventRecord(c->ev[2], s));
-            HIPCHK(hipEventSynchronize(c->ev[2]));
-            float a;
-            hipEventElapsedTime(&a, c->ev[1], c->ev[2]);
-            t_copy += a;
-        }
+        if ((rc = mark(4))) return rc;
         g0 = g1;
     }
     so[n_streams] = total;
     HIPCHK(hipMemcpyAsync(c->stream_off.p, so.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     if (c->timing) {
-        c->last.front_ms = t_front;
-        c->last.alloc_ms = t_alloc;
-        c->last.scan_ms = t_copy;
-        c->last.pack_ms = t_pack;
-        c->last.total_ms = t_front + t_alloc + t_copy + t_pack;
+        float ph[5] = {0, 0, 0, 0, 0};
+        for (size_t i = 1; i < marks.size(); i++) {
+            if (marks[i].second < 0) continue;
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, c->evpool[marks[i - 1].first], c->evpool[marks[i].first]));
+            ph[marks[i].second] += ms;
+        }
+        c->last.thr_ms = ph[0];
+        c->last.front_ms = ph[1];
+        c->last.alloc_ms = ph[2];
+        c->last.pack_ms = ph[3];
+        c->last.scan_ms = ph[4];
+        c->last.total_ms = ph[0] + ph[1] + ph[2] + ph[3] + ph[4];
         c->last.n_channel_blocks = 2 * blk[n_streams];
         c->last.out_bytes = total;
     }
@@ -800,8 +815,14 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     }
     HIPCHK(hipMemcpyAsync(stream_byte_offsets, c->stream_off.p, (n_streams + 1) * sizeof(int64_t),
                           hipMemcpyDeviceToHost, s));
-    if (!out_is_device && total) HIPCHK(hipMemcpyAsync(out, out_dev, total, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (total > out_capacity)
+        return set_err(PAC_E_CAPACITY, "output needs %lld bytes, capacity %lld", (long long)total,
+                       (long long)out_capacity);
+    if (!out_is_device && total) {
+        HIPCHK(hipMemcpyAsync(out, out_dev, total, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     if (!master) finish_timing(c, G, total);
     return PAC_OK;
 }
@@ -875,6 +896,7 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
         int64_t* off_dev = nullptr;
         if ((rc = run_origin(c, p, T, src, G, c->out_stage.p, c->out_stage.n, &total, &off_dev))) return rc;
         HIPCHK(hipMemcpyAsync(smr.data(), c->smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
         finish_timing(c, G, total);
     }
     if (total > out_capacity) return set_err(PAC_E_CAPACITY, "block needs %lld bytes", (long long)total);

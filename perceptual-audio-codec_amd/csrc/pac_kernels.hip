@@ -442,7 +442,7 @@ __device__ __forceinline__ void store_block_bytes(uint8_t* __restrict__ out, con
 __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const PacTables* __restrict__ T,
                                                           PacOriginWork W, int64_t G,
                                                           const int64_t* __restrict__ off,
-                                                          uint8_t* __restrict__ out) {
+                                                          uint8_t* __restrict__ out, int64_t cap) {
     __shared__ double2 buf[1024];        // MDCT: lines in the first 8 KB
     __shared__ uint32_t words[PACK_WORDS];
     __shared__ int start[PAC_NB];
@@ -483,6 +483,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
     }
     __syncthreads();
     const int nbytes = W.nbytes[g] - 4;
+    if (off[g] + 4 + nbytes > cap) return;     // host reports PAC_E_CAPACITY from the total
     uint8_t* o = out + off[g];
     if (tid < 4) o[tid] = (uint8_t)((uint32_t)nbytes >> (8 * tid));   // '<L' nBytes
     for (int i = tid; i < nbytes; i += FRONT_NT) o[4 + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));

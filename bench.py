@@ -400,7 +400,7 @@ PHASES = {  # pac_timing field -> kernel, per profile (include/pac_gpu.h)
     "origin": [("front_ms", "k_origin_front"), ("alloc_ms", "k_origin_alloc"), ("scan_ms", "k_scan"),
                ("pack_ms", "k_origin_pack")],
     "master": [("thr_ms", "k_master_thr"), ("front_ms", "k_master_front"), ("alloc_ms", "k_master_tail"),
-               ("pack_ms", "k_master_pack"), ("scan_ms", "k_copy_streams")],
+               ("pack_ms", "k_master_pack"), ("scan_ms", "k_scan")],
 }
 
 

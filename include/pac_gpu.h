@@ -61,14 +61,15 @@ typedef struct {
  * context's stream around each launch, read after the call), ms.
  *   origin: front = k_origin_front, alloc = k_origin_alloc, scan = k_scan_*,
  *           pack = k_origin_pack, thr = 0
- *   master: thr = k_master_thr, front = k_master_front, alloc = k_master_tail,
- *           pack = k_master_pack, scan = k_copy_streams (summed over chunks) */
+ *   master: thr = k_master_thr, front = k_master_front, alloc = k_master_tail
+ *           (second stream, overlapping the next chunk), scan = k_scan_*,
+ *           pack = k_master_pack (each summed over the call's chunks) */
 typedef struct {
     float front_ms;
     float alloc_ms;
     float scan_ms;
     float pack_ms;
-    float total_ms;     /* sum of the phases (master) / first to last event (origin) */
+    float total_ms;     /* origin: first to last event; master: thr+front+scan+pack */
     int64_t n_channel_blocks;
     int64_t out_bytes;
     float thr_ms;
@@ -86,6 +87,12 @@ typedef struct {
     int32_t lrms[25];            /* LRMS[iBand] (master)                        */
     int32_t nbytes[8];           /* payload bytes of the channel-block          */
     double smr[8][25];           /* SMR fed to BitAlloc                         */
+    /* master: huffmanCodedMantissa[iCh] (codec.py:111-129, Huffman.py:274-309)
+     * by MDCT line: the code's bits (an escape is the escape code followed by
+     * the ba raw bits of the unsigned mantissa, Huffman.py:296-299) right-aligned,
+     * and its length in bits (0 for lines of ba = 0 bands)                   */
+    uint64_t huff_code[8][1024];
+    int32_t huff_len[8][1024];
 } pac_block_fields;
 
 /* --- context ------------------------------------------------------------ */

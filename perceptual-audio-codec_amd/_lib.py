@@ -47,7 +47,8 @@ class BlockFields(C.Structure):
                 ("ba", (C.c_int32 * 25) * 8), ("sf", (C.c_int32 * 25) * 8),
                 ("mant", (C.c_int32 * 1024) * 8), ("table_id", C.c_int32 * 8),
                 ("lrms", C.c_int32 * 25), ("nbytes", C.c_int32 * 8),
-                ("smr", (C.c_double * 25) * 8)]
+                ("smr", (C.c_double * 25) * 8),
+                ("huff_code", (C.c_uint64 * 1024) * 8), ("huff_len", (C.c_int32 * 1024) * 8)]
 
 
 _lib = None

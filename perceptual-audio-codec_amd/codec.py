@@ -65,22 +65,28 @@ def Encode(data, codingParams, huffman=None, profile=PROFILE_MASTER, context=Non
     """codec.Encode: the block's coded fields, as the reference returns them."""
     raw, f = _run(data, codingParams, huffman, profile, context)
     nch = codingParams.nChannels
-    nl = codingParams.sfBands.nLines if hasattr(codingParams, "sfBands") else None
+    nl = np.asarray(codingParams.sfBands.nLines if hasattr(codingParams, "sfBands")
+                    else _lib.band_layout(codingParams.sampleRate), dtype=np.int64)
     scaleFactor = [np.array(f.sf[c][:], dtype=np.int32) for c in range(nch)]
     bitAlloc = [np.array(f.ba[c][:], dtype=np.int64) for c in range(nch)]
     overall = [int(f.overall[c]) for c in range(nch)]
     mant = []
     for c in range(nch):
         m = np.array(f.mant[c][:], dtype=np.int32)
-        keep = np.repeat(bitAlloc[c] > 0, nl) if nl is not None else m != 0
-        mant.append(m[keep])
+        mant.append(m[:nl.sum()][np.repeat(bitAlloc[c] > 0, nl)])
     if profile == PROFILE_ORIGIN:
         return scaleFactor, bitAlloc, mant, overall
+    # StripSignBits (codec.py:67-81) and huffman.encodeData's code strings
+    # (Huffman.py:274-309) as the GPU pack kernel emitted them, one per coded
+    # line in band order -- what PACFile.WriteDataBlock consumes (pacfile.py:296-336)
     signBits, huffCoded = [], []
     for c in range(nch):
-        ba = np.repeat(bitAlloc[c], nl)[np.repeat(bitAlloc[c] > 0, nl)]
+        keep = np.repeat(bitAlloc[c] > 0, nl)
+        ba = np.repeat(bitAlloc[c], nl)[keep]
         signBits.append([int(v >> (b - 1)) & 1 for v, b in zip(mant[c], ba)])
-        huffCoded.append(None)   # codes are emitted straight into the bitstream
+        codes = np.array(f.huff_code[c][:], dtype=np.uint64)[:nl.sum()][keep]
+        lens = np.array(f.huff_len[c][:], dtype=np.int64)[:nl.sum()][keep]
+        huffCoded.append([format(int(v), "0%db" % n) for v, n in zip(codes, lens)])
     tableID = [int(f.table_id[c]) for c in range(nch)]
     LRMS = np.array(f.lrms[:], dtype=np.int64)
     return scaleFactor, bitAlloc, signBits, huffCoded, tableID, overall, LRMS

@@ -241,11 +241,12 @@ struct pac_ctx {
     // master
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
-    DevBuf<int64_t> st_extra, st_deposit, st_cursor, m_src_off, m_dst_off, m_size;
-    DevBuf<uint8_t> m_stage;                // master: packed bytes of a stream group before the copy
-    int64_t stage_max = (int64_t)16 << 30;  // bytes of worst-case output per stream group
-    PacHuffTables* huff_host = nullptr;
-    std::unordered_map<uint64_t, int> huff_dec[PAC_NTAB];   // (len<<32|code) -> symbol, -1 = escape
+    DevBuf<int64_t> st_extra, st_deposit;
+    DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
+    DevBuf<uint64_t> dbg_code;
+    DevBuf<uint8_t> dbg_len;
+    hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
+    hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
     DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)
     PacHuffDec hdec = {};
@@ -254,7 +255,7 @@ struct pac_ctx {
     DevBuf<int64_t> dec_so, dec_cnt, dec_cbbase, dec_cboff, dec_nblk, dec_segbase, dec_fo;
     DevBuf<int16_t> dec_pcm;
     DevBuf<double> dec_fpcm;
-    int64_t chunk_blocks = 32768;
+    int64_t chunk_blocks = 65536;
     int dbg = 0;                           // PAC_DEBUG_FLAGS (diagnostic builds of the timing only)
     // timing
     bool timing = false;
@@ -279,11 +280,13 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     HIPCHK(hipSetDevice(device));
     pac_ctx* c = new pac_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
     }
     for (auto& e : c->ev) hipEventCreate(&e);
+    for (auto& e : c->evs) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (const char* f = getenv("PAC_DEBUG_FLAGS")) c->dbg = atoi(f);
     *out = c;
     return PAC_OK;
@@ -293,13 +296,13 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(c->stream2);
     for (auto& kv : c->tables) hipFree(kv.second);
     if (c->huff) hipFree(c->huff);
-    free(c->huff_host);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
-    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->st_cursor.release();
-    c->m_src_off.release(); c->m_dst_off.release(); c->m_size.release(); c->m_stage.release();
+    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release();
+    c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
     c->dec_ov.release(); c->dec_lrms.release(); c->dec_codes.release(); c->dec_so.release();
     c->dec_cnt.release(); c->dec_cbbase.release(); c->dec_cboff.release(); c->dec_nblk.release();
@@ -310,7 +313,9 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->stream_off.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
     for (auto& e : c->ev) hipEventDestroy(e);
     for (auto& e : c->evpool) hipEventDestroy(e);
+    for (auto& e : c->evs) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
+    hipStreamDestroy(c->stream2);
     delete c;
 }
 
@@ -384,22 +389,20 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
     }
     int rc2;
     hipError_t e = hipMemcpy(c->huff, h, sizeof(PacHuffTables), hipMemcpyHostToDevice);
-    free(c->huff_host);
-    c->huff_host = h;    // kept for pac_encode_block's field reconstruction
-    for (int t = 0; t < PAC_NTAB; t++) {
-        c->huff_dec[t].clear();
-        for (int sym = 0; sym < PAC_NSYM; sym++)
-            if (h->len[t][sym]) c->huff_dec[t][((uint64_t)h->len[t][sym] << 32) | h->bits[t][sym]] = sym;
-        c->huff_dec[t][((uint64_t)h->esc_len[t] << 32) | h->esc_bits[t]] = -1;
+    if (e != hipSuccess) {
+        free(h);
+        return set_err(PAC_E_HIP, "huffman upload: %s", hipGetErrorString(e));
     }
-    if (e != hipSuccess) return set_err(PAC_E_HIP, "huffman upload: %s", hipGetErrorString(e));
     // decoding tables (Huffman.decodeData, Huffman.py:321-344): level 1 on the
     // first min(11, maxlen) bits, level 2 for longer codes
     std::vector<uint32_t> tab;
     for (int t = 0; t < PAC_NTAB; t++) {
         int ml = h->esc_len[t];
         for (int sym = 0; sym < PAC_NSYM; sym++) ml = std::max(ml, (int)h->len[t][sym]);
-        if (ml > 30) return set_err(PAC_E_TABLES, "code longer than 30 bits");
+        if (ml > 30) {
+            free(h);
+            return set_err(PAC_E_TABLES, "code longer than 30 bits");
+        }
         const int l1 = std::min(ml, 11), l2 = ml - l1;
         const size_t base = tab.size();
         tab.resize(base + ((size_t)1 << l1), 0u);
@@ -429,6 +432,7 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
         c->hdec.maxlen[t] = ml;
         c->hdec.l1[t] = l1;
     }
+    free(h);
     if ((rc2 = c->hdec_tab.ensure(tab.size()))) return rc2;
     HIPCHK(hipMemcpy(c->hdec_tab.p, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->have_huff = true;
@@ -603,143 +607,134 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     c->last.out_bytes = bytes;
 }
 
-// --- master: chunks of whole-block ranges, stream-major ----------------------
+// --- master: two passes, chunks of whole-block ranges ---------------------
 
 // Runs the master pipeline over global blocks [0, nblocks).  States (device
-// st_extra / st_deposit, per stream) must be initialised by the caller.
-// Master profile.  Streams are taken in groups whose worst-case output fits
-// the staging area (c->stage_max) and whose size is at most c->chunk_blocks;
-// each group is swept in time slices of S blocks per stream (S * streams <=
-// chunk_blocks), so every stream's serial reservoir chain advances in
-// parallel.  Packed channel-blocks land in staging at each stream's running
-// cursor; after the group, k_copy_streams moves every stream to its final
-// offset.  Fills c->stream_off (n_streams + 1 entries) on the device.
+// st_extra / st_deposit, per stream) must be initialised by the caller on
+// c->stream.  Pass 1: streams in groups of at most chunk_blocks, each group
+// swept in time slices of S blocks per stream (S * streams <= chunk_blocks)
+// so every stream's serial reservoir chain advances in parallel; thresholds +
+// front on c->stream, the tail of the same chunk on c->stream2 while the next
+// chunk's thresholds run (chunk outputs double-buffered, ordered by events).
+// Pass 2: exclusive scan of the channel-block byte counts (file order) ->
+// final offsets, then k_master_pack writes every channel-block in place.
+// No host synchronisation inside the pipeline.  Leaves the offsets in c->off
+// and the total (async) in *out_total.
 static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src,
                       const std::vector<int64_t>& blk, uint8_t* out_dev, int64_t out_cap,
-                      int64_t* out_total) {
+                      int64_t* out_total, bool dbg_codes) {
     int rc;
     const int n_streams = src.n_streams;
+    const int64_t nblocks = blk[n_streams];
+    const int64_t G = 2 * nblocks;
     const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : 1;
-    const int64_t per = pac_encode_bound_per_channel_block();
-    std::vector<int64_t> lens(n_streams);
-    int64_t maxlen = 0;
-    for (int s = 0; s < n_streams; s++) {
-        lens[s] = blk[s + 1] - blk[s];
-        if (lens[s] > maxlen) maxlen = lens[s];
-    }
-    if ((rc = c->st_cursor.ensure(n_streams)) || (rc = c->m_src_off.ensure(n_streams)) ||
-        (rc = c->m_dst_off.ensure(n_streams)) || (rc = c->m_size.ensure(n_streams)))
-        return rc;
-    hipStream_t s = c->stream;
-    const double budget = bit_budget(p);
-    // timing: events recorded around every launch, read once after the call
-    // (no host round trip inside the pipeline); marks[i] = (event, phase)
-    std::vector<std::pair<size_t, int>> marks;
-    size_t nev = 0;
-    auto mark = [&](int phase) -> int {
-        if (!c->timing) return PAC_OK;
-        const hipEvent_t e = c->pool_event(nev);
-        marks.emplace_back(nev++, phase);
-        HIPCHK(hipEventRecord(e, s));
-        return PAC_OK;
-    };
-    std::vector<int64_t> so(n_streams + 1, 0), src_off(n_streams), cursor(n_streams), dst(n_streams),
-        size(n_streams);
-    int64_t total = 0;
+    // chunk geometry: group [g0, g1) of at most CB streams, S blocks each
+    struct Grp { int g0, n_s, S; int64_t gmax; };
+    std::vector<Grp> groups;
+    int64_t cbmax = 1;
     for (int g0 = 0; g0 < n_streams;) {
-        // --- the group [g0, g1)
-        int64_t bound = 0, gmax = 0;
-        int g1 = g0;
-        while (g1 < n_streams) {
-            const int64_t b = lens[g1] * 2 * per;
-            if (g1 > g0 && (bound + b > c->stage_max || (int64_t)(g1 - g0) >= CB)) break;
-            src_off[g1] = bound;
-            bound += b;
-            if (lens[g1] > gmax) gmax = lens[g1];
-            g1++;
-        }
+        const int g1 = (int)std::min<int64_t>(n_streams, g0 + CB);
+        int64_t gmax = 1;
+        for (int k = g0; k < g1; k++) gmax = std::max<int64_t>(gmax, blk[k + 1] - blk[k]);
         const int n_s = g1 - g0;
-        // slice length: S blocks of each stream per chunk, never past the longest
-        int64_t S64 = CB / n_s;
-        if (S64 > gmax) S64 = gmax;
-        if (S64 < 1) S64 = 1;
-        const int S = (int)S64;
-        const int64_t cb = (int64_t)n_s * S;          // local blocks per chunk
-        HIPCHK(hipStreamSynchronize(s));              // nothing in flight before any re-allocation
-        if ((rc = c->m_stage.ensure(bound > 0 ? bound : 1)) || (rc = c->m_thr.ensure(cb * 6 * PAC_HALFN)) ||
-            (rc = c->m_lines.ensure(cb * 2 * PAC_HALFN)) || (rc = c->m_smr.ensure(cb * 2 * PAC_NB)) ||
-            (rc = c->m_peak.ensure(cb * 2 * PAC_NB)) || (rc = c->m_lrms.ensure(cb * PAC_NB)) ||
-            (rc = c->m_overall.ensure(cb * 2)) || (rc = c->m_ba.ensure(cb * 2 * PAC_NB)) ||
-            (rc = c->m_sf.ensure(cb * 2 * PAC_NB)) || (rc = c->m_tid.ensure(cb * 2)) ||
-            (rc = c->nbytes.ensure(cb * 2)) || (rc = c->off.ensure(cb * 2 + 1)))
-            return rc;
-        const PacMasterWork W{c->m_thr.p, c->m_lines.p, c->m_smr.p, c->m_peak.p, c->m_lrms.p, c->m_overall.p,
-                              c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p};
-        HIPCHK(hipMemcpyAsync(c->st_cursor.p + g0, src_off.data() + g0, n_s * sizeof(int64_t),
-                              hipMemcpyHostToDevice, s));
-        for (int64_t t0 = 0; t0 < gmax; t0 += S) {
-            const PacMasterChunk ck{g0, n_s, t0, S};
-            const int64_t B = (int64_t)n_s * S;
-            if ((rc = mark(-1))) return rc;
-            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s, src, T, W, ck);
-            if ((rc = mark(0))) return rc;
-            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s, src, T, W, ck);
-            HIPCHK(hipGetLastError());
-            if ((rc = mark(1))) return rc;
-            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)n_s), dim3(64), 0, s, T, c->huff, W, c->blk_off.p, ck,
-                               c->st_extra.p, c->st_deposit.p, c->st_cursor.p, c->off.p, budget);
-            HIPCHK(hipGetLastError());
-            if ((rc = mark(2))) return rc;
-            hipLaunchKernelGGL(k_master_pack, dim3((unsigned)(2 * B)), dim3(64), 0, s, T, c->huff, W,
-                               c->blk_off.p, ck, c->off.p, c->m_stage.p);
-            HIPCHK(hipGetLastError());
-            if ((rc = mark(3))) return rc;
-        }
-        // --- final offsets of the group's streams, then the copy
-        HIPCHK(hipMemcpyAsync(cursor.data() + g0, c->st_cursor.p + g0, n_s * sizeof(int64_t),
-                              hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        for (int k = g0; k < g1; k++) {
-            size[k] = cursor[k] - src_off[k];
-            dst[k] = total;
-            so[k] = total;
-            total += size[k];
-        }
-        if (total > out_cap)
-            return set_err(PAC_E_CAPACITY, "output needs > %lld bytes, capacity %lld", (long long)total,
-                           (long long)out_cap);
-        HIPCHK(hipMemcpyAsync(c->m_src_off.p + g0, src_off.data() + g0, n_s * sizeof(int64_t),
-                              hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->m_dst_off.p + g0, dst.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->m_size.p + g0, size.data() + g0, n_s * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if ((rc = mark(-1))) return rc;
-        hipLaunchKernelGGL(k_copy_streams, dim3((unsigned)n_s), dim3(256), 0, s, c->m_stage.p, c->m_src_off.p + g0,
-                           c->m_dst_off.p + g0, c->m_size.p + g0, out_dev);
-        HIPCHK(hipGetLastError());
-        if ((rc = mark(4))) return rc;
+        const int S = (int)std::max<int64_t>(1, std::min<int64_t>(CB / n_s, gmax));
+        groups.push_back({g0, n_s, S, gmax});
+        cbmax = std::max<int64_t>(cbmax, (int64_t)n_s * S);
         g0 = g1;
     }
-    so[n_streams] = total;
-    HIPCHK(hipMemcpyAsync(c->stream_off.p, so.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (c->timing) {
-        float ph[5] = {0, 0, 0, 0, 0};
-        for (size_t i = 1; i < marks.size(); i++) {
-            if (marks[i].second < 0) continue;
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, c->evpool[marks[i - 1].first], c->evpool[marks[i].first]));
-            ph[marks[i].second] += ms;
+    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
+        (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
+        (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
+        (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
+        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_lines.ensure(2 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_smr.ensure(2 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(2 * cbmax * 2 * PAC_NB)))
+        return rc;
+    PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
+                      nullptr, nullptr, nullptr};
+    if (dbg_codes) {
+        if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
+            (rc = c->dbg_len.ensure(G * PAC_HALFN)))
+            return rc;
+        F.dbg_mant = c->dbg_mant.p;
+        F.dbg_code = c->dbg_code.p;
+        F.dbg_len = c->dbg_len.p;
+    }
+    hipStream_t s0 = c->stream, s1 = c->stream2;
+    const double budget = bit_budget(p);
+    // timing: events recorded around every launch on its own stream, read
+    // once after the call; mk[k] = (pool event, phase) of stream k, phase -1
+    // opens an interval, phase >= 0 closes one
+    std::vector<std::pair<size_t, int>> mk[2];
+    size_t nev = 0;
+    auto mark = [&](int k, int phase) -> int {
+        if (!c->timing) return PAC_OK;
+        const hipEvent_t e = c->pool_event(nev);
+        mk[k].emplace_back(nev++, phase);
+        HIPCHK(hipEventRecord(e, k ? s1 : s0));
+        return PAC_OK;
+    };
+    HIPCHK(hipEventRecord(c->evs[4], s0));            // states and tables are on s0
+    HIPCHK(hipStreamWaitEvent(s1, c->evs[4], 0));
+    int64_t i = 0;
+    for (const Grp& gr : groups) {
+        for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S, ++i) {
+            const int k = (int)(i & 1);
+            const PacMasterChunk ck{gr.g0, gr.n_s, t0, gr.S};
+            const PacMasterChunkBuf K{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
+                                      c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB};
+            const int64_t B = (int64_t)gr.n_s * gr.S;
+            if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
+            if ((rc = mark(0, -1))) return rc;
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s0, src, T, K, ck);
+            if ((rc = mark(0, 0))) return rc;
+            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
+            HIPCHK(hipGetLastError());
+            if ((rc = mark(0, 1))) return rc;
+            HIPCHK(hipEventRecord(c->evs[k], s0));
+            HIPCHK(hipStreamWaitEvent(s1, c->evs[k], 0));
+            if ((rc = mark(1, -1))) return rc;
+            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)gr.n_s), dim3(64), 0, s1, T, c->huff, K, F,
+                               c->blk_off.p, ck, c->st_extra.p, c->st_deposit.p, budget);
+            HIPCHK(hipGetLastError());
+            if ((rc = mark(1, 2))) return rc;
+            HIPCHK(hipEventRecord(c->evs[2 + k], s1));
         }
+    }
+    HIPCHK(hipEventRecord(c->evs[4], s1));
+    HIPCHK(hipStreamWaitEvent(s0, c->evs[4], 0));
+    // pass 2: byte offsets in file order, then the packing
+    if ((rc = mark(0, -1))) return rc;
+    const int64_t ntiles = (G + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(256), 0, s0, c->nbytes.p, G, c->tile_sums.p);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s0, c->tile_sums.p, ntiles, c->grand_total.p);
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(256), 0, s0, c->nbytes.p, G, c->tile_sums.p,
+                       c->off.p);
+    HIPCHK(hipGetLastError());
+    if ((rc = mark(0, 4))) return rc;
+    hipLaunchKernelGGL(k_master_pack, dim3((unsigned)nblocks), dim3(256), 0, s0, src, T, c->huff, F, nblocks,
+                       c->off.p, out_dev, out_cap);
+    HIPCHK(hipGetLastError());
+    if ((rc = mark(0, 3))) return rc;
+    HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s0));
+    if (c->timing) {
+        HIPCHK(hipStreamSynchronize(s0));
+        float ph[5] = {0, 0, 0, 0, 0};
+        for (int k = 0; k < 2; k++)
+            for (size_t j = 1; j < mk[k].size(); j++) {
+                if (mk[k][j].second < 0) continue;
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, c->evpool[mk[k][j - 1].first], c->evpool[mk[k][j].first]));
+                ph[mk[k][j].second] += ms;
+            }
         c->last.thr_ms = ph[0];
         c->last.front_ms = ph[1];
         c->last.alloc_ms = ph[2];
         c->last.pack_ms = ph[3];
         c->last.scan_ms = ph[4];
-        c->last.total_ms = ph[0] + ph[1] + ph[2] + ph[3] + ph[4];
-        c->last.n_channel_blocks = 2 * blk[n_streams];
-        c->last.out_bytes = total;
+        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4];   // the tail overlaps the next chunk
+        c->last.n_channel_blocks = G;
+        c->last.out_bytes = 0;
     }
-    *out_total = total;
     return PAC_OK;
 }
 
@@ -799,7 +794,10 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
             for (int i = 0; i < n_streams; i++) { ex[i] = states[i].extra_bits; dp[i] = states[i].bit_deposit; }
         HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total))) return rc;
+        if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false))) return rc;
+        hipLaunchKernelGGL(k_stream_offsets, dim3((n_streams + 1 + 255) / 256), dim3(256), 0, s, c->off.p,
+                           c->blk_off.p, n_streams, nch, c->grand_total.p, c->stream_off.p);
+        HIPCHK(hipGetLastError());
         if (states) {
             HIPCHK(hipMemcpyAsync(ex.data(), c->st_extra.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(dp.data(), c->st_deposit.p, n_streams * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -839,21 +837,6 @@ struct BitReader {
     }
 };
 
-// Huffman.decodeData (Huffman.py:321-344) on the host copy of the tables, used
-// only to hand the codec.Encode() tuple back to the plugin surface.
-static uint32_t host_huff_decode(const std::unordered_map<uint64_t, int>& dec, const PacHuffTables* h,
-                                 int tid, BitReader& br, int ba) {
-    uint32_t code = 0;
-    for (int len = 1; len <= 32; len++) {
-        code = (code << 1) | br.get(1);
-        auto it = dec.find(((uint64_t)len << 32) | code);
-        if (it != dec.end()) return it->second < 0 ? br.get(ba) : (uint32_t)it->second;
-    }
-    (void)h;
-    (void)tid;
-    return 0;
-}
-
 extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* full_block,
                                 pac_stream_state* state, uint8_t* out, int64_t out_capacity, int64_t* out_bytes,
                                 pac_block_fields* fields) {
@@ -876,6 +859,9 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
     int64_t total = 0;
     std::vector<double> smr(PAC_NB * G);
     int32_t lrms[PAC_NB] = {0};
+    std::vector<uint32_t> dbg_mant;
+    std::vector<uint64_t> dbg_code;
+    std::vector<uint8_t> dbg_len;
     if (master) {
         std::vector<int64_t> blk = {0, 1};
         HIPCHK(hipMemcpyAsync(c->blk_off.p, blk.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, s));
@@ -883,7 +869,18 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
         int64_t ex = state ? state->extra_bits : 0, dp = state ? state->bit_deposit : 0;
         HIPCHK(hipMemcpyAsync(c->st_extra.p, &ex, sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->st_deposit.p, &dp, sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if ((rc = run_master(c, p, T, src, blk, c->out_stage.p, c->out_stage.n, &total))) return rc;
+        if ((rc = run_master(c, p, T, src, blk, c->out_stage.p, c->out_stage.n, &total, fields != nullptr)))
+            return rc;
+        if (fields) {   // per-line mantissas and Huffman codes as the pack kernel emitted them
+            dbg_mant.resize(2 * PAC_HALFN);
+            dbg_code.resize(2 * PAC_HALFN);
+            dbg_len.resize(2 * PAC_HALFN);
+            HIPCHK(hipMemcpyAsync(dbg_mant.data(), c->dbg_mant.p, 2 * PAC_HALFN * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(dbg_code.data(), c->dbg_code.p, 2 * PAC_HALFN * sizeof(uint64_t),
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(dbg_len.data(), c->dbg_len.p, 2 * PAC_HALFN, hipMemcpyDeviceToHost, s));
+        }
         HIPCHK(hipMemcpyAsync(&ex, c->st_extra.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&dp, c->st_deposit.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(smr.data(), c->m_smr.p, smr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -904,7 +901,9 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
     HIPCHK(hipStreamSynchronize(s));
     *out_bytes = total;
     if (fields) {
-        // the codec.Encode() tuple, read back from the GPU-written channel-blocks
+        // the codec.Encode() tuple: side info read back from the GPU-written
+        // channel-blocks, mantissas (origin: raw codes in the bitstream;
+        // master: as the pack kernel emitted them, with their Huffman codes)
         memset(fields, 0, sizeof(*fields));
         fields->n_channels = nch;
         int32_t nl[PAC_NB];
@@ -926,12 +925,13 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
                 fields->smr[ch][b] = smr[ch * PAC_NB + b];
                 if (!master) {
                     for (int l = 0; l < nl[b]; l++) fields->mant[ch][line + l] = ba ? (int32_t)br.get(ba) : 0;
-                } else if (ba) {
-                    uint32_t sg[1024];
-                    for (int l = 0; l < nl[b]; l++) sg[l] = br.get(1);
-                    for (int l = 0; l < nl[b]; l++) {
-                        uint32_t mag = host_huff_decode(c->huff_dec[tid - 1], c->huff_host, tid - 1, br, ba);
-                        fields->mant[ch][line + l] = (int32_t)(mag + (sg[l] << (ba - 1)));
+                } else if (ba) {      // skip the band's sign bits and codes in the bitstream
+                    br.bit += nl[b];
+                    for (int l = line; l < line + nl[b]; l++) {
+                        fields->mant[ch][l] = (int32_t)dbg_mant[ch * PAC_HALFN + l];
+                        fields->huff_code[ch][l] = dbg_code[ch * PAC_HALFN + l];
+                        fields->huff_len[ch][l] = (int32_t)dbg_len[ch * PAC_HALFN + l];
+                        br.bit += dbg_len[ch * PAC_HALFN + l];
                     }
                 }
                 line += nl[b];

@@ -1,35 +1,51 @@
 // pac_master.hip -- gfx950 kernels of the master (.wak) profile: codec/ of the
 // reference (M/S decision, six masking thresholds, bit reservoir, Huffman).
 //
-// Streams are processed in groups; a group is swept in time slices (chunk =
-// blocks t0..t0+S-1 of every stream of the group, PacMasterChunk), so the
-// serial reservoir chain of every stream of the group advances in parallel:
-//   k_master_thr    one wave per (block, variant): the six calcBTHR() calls of
-//                   getStereoMaskThreshold (psychoac.py:540-562) incl. the
-//                   in-place Hann chains -> thr[gb][v][1024]
-//   k_master_front  one wave per block: LRMS decision (codec.py:94-102), MDCT
-//                   L/R + overall scale (codec.py:237-246), M/S lines, MLD
+// Two passes over the call's blocks (file order: stream, block, channel).
+// Pass 1 sweeps time slices (chunk = blocks t0..t0+S-1 of every stream of a
+// stream group, PacMasterChunk) so the serial reservoir chain of every stream
+// advances in parallel; pass 2 packs every channel-block at its final offset:
+//   k_master_thr    one workgroup per (block, variant): the six calcBTHR()
+//                   calls of getStereoMaskThreshold (psychoac.py:540-562) incl.
+//                   the in-place Hann chains -> chunk thr[j][v][1024]
+//   k_master_front  one workgroup per block: LRMS decision (codec.py:94-102),
+//                   MDCT L/R + overall scale (codec.py:237-246), M/S lines, MLD
 //                   combination and per-band SMR selection (psychoac.py:533-682)
-//   k_master_tail   one wave per STREAM of the chunk, its blocks in order: withdrawBits, the two
-//                   BitAlloc calls with the extraBits carry (codec.py:222-260,
-//                   bitalloc.py:129-184), scale factors, 10-table Huffman
-//                   length scoring and depositBits (codec.py:111-124)
-//   k_master_pack   one wave per channel-block: sign bits, Huffman codes and
-//                   LRMS packed MSB-first (pacfile.py:288-351) into the
-//                   group's staging area at the stream's running cursor
-//   k_copy_streams  after a group: each stream's bytes to its final offset
+//   k_master_tail   one wave per STREAM of the chunk, its blocks in order:
+//                   withdrawBits, the two BitAlloc calls with the extraBits carry
+//                   (codec.py:222-260, bitalloc.py:129-184), scale factors,
+//                   10-table Huffman length scoring, depositBits (codec.py:111-124)
+//                   and the channel-block's byte count
+//   (k_scan_* over the byte counts -> final offsets, as the origin profile)
+//   k_master_pack   one workgroup per block (pass 2): MDCT L/R recomputed from
+//                   the PCM (cheaper than keeping 16 KB of lines per block in
+//                   HBM), M/S lines, sign bits, Huffman codes and LRMS packed
+//                   MSB-first (pacfile.py:288-351) straight to the final offset.
+// The tail of chunk i runs on a second HIP stream, concurrently with the
+// threshold/front kernels of chunk i+1 (double-buffered chunk outputs).
 
-struct PacMasterWork {
+// chunk-local scratch, local block j (thr single-buffered: written and read on
+// the front stream; the rest double-buffered between front and tail)
+struct PacMasterChunkBuf {
     double* thr;        // [Bc][6][1024]
     double* lines;      // [Bc][2][1024]  LRMSmdctLines
     double* smr;        // [Bc][2][25]
-    double* bandpeak;   // [Bc][2][25]
-    uint8_t* lrms;      // [Bc][25]
-    uint8_t* overall;   // [Bc][2]
-    uint8_t* ba;        // [Bc][2][25]
-    uint8_t* sf;        // [Bc][2][25]
-    uint8_t* tid;       // [Bc][2]
-    int32_t* nbytes;    // [Bc*2]
+    double* bandpeak;   // [Bc][2][25]    max |line| per band
+};
+
+// per-call fields; channel-block g = 2 gb + ch (gb = global block, file order)
+struct PacMasterFields {
+    uint8_t* lrms;      // [nblocks][25]
+    uint8_t* overall;   // [G]
+    uint8_t* ba;        // [G][25]
+    uint8_t* sf;        // [G][25]
+    uint8_t* tid;       // [G]
+    int32_t* nbytes;    // [G]  '<L' + payload bytes
+    // per-block API only (else null): per MDCT line of g, the signed mantissa
+    // code, its Huffman code (escape code ++ ba raw bits for an escape) and length
+    uint32_t* dbg_mant;  // [G][1024]
+    uint64_t* dbg_code;  // [G][1024]
+    uint8_t* dbg_len;    // [G][1024]
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of streams
@@ -68,7 +84,7 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 }
 
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                         PacMasterWork W, PacMasterChunk ck) {
+                                                         PacMasterChunkBuf K, PacMasterChunk ck) {
     __shared__ double2 buf[1024];
     __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // FFT / peak scratch, then beta rows
     __shared__ int16_t rank[PAC_HALFN];
@@ -85,7 +101,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta), rank);
-    double* out = W.thr + (j * 6 + v) * PAC_HALFN;
+    double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));
     if (tid == 0) *rowctr = 0;
@@ -179,7 +195,8 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 // overall scales, M/S lines, MLD threshold combination, SMR selection and the
 // band maxima (LDS atomic max on order-preserving keys).
 __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
-                                                      PacMasterWork W, PacMasterChunk ck) {
+                                                      PacMasterChunkBuf K, PacMasterFields F,
+                                                      PacMasterChunk ck) {
     __shared__ double2 bufA[1024], bufB[1024], bufC[1024];    // 48 KB
     __shared__ double2 leafv[2][64];
     __shared__ uint8_t lrms_s[PAC_NB];
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         const double2 ss = np_csum_combine<5>(leafv[1], i1, n);
         const int v = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
         lrms_s[tid] = (uint8_t)v;
-        W.lrms[j * PAC_NB + tid] = (uint8_t)v;
+        F.lrms[gb * PAC_NB + tid] = (uint8_t)v;
     }
     __syncthreads();
 
@@ -244,11 +261,11 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
     const double gL = (double)(1 << oL), gR = (double)(1 << oR);
     const double offL = 6.02 * oL, offR = 6.02 * oR;
-    if (tid == 0) { W.overall[j * 2] = (uint8_t)oL; W.overall[j * 2 + 1] = (uint8_t)oR; }
+    if (tid == 0) { F.overall[gb * 2] = (uint8_t)oL; F.overall[gb * 2 + 1] = (uint8_t)oR; }
 
     // --- per-line SMR terms (psychoac.py:533-597), selection (:662-682) ----
-    const double* thr = W.thr + j * 6 * PAC_HALFN;
-    double* lines = W.lines + j * 2 * PAC_HALFN;
+    const double* thr = K.thr + j * 6 * PAC_HALFN;
+    double* lines = K.lines + j * 2 * PAC_HALFN;
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -287,10 +304,10 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     __syncthreads();
     if (tid < PAC_NB) {
         const bool has = T->nlines[tid] != 0;
-        W.smr[(j * 2 + 0) * PAC_NB + tid] = has ? pac_order_unkey(key[0][tid]) : -96.0;
-        W.smr[(j * 2 + 1) * PAC_NB + tid] = has ? pac_order_unkey(key[1][tid]) : -96.0;
-        W.bandpeak[(j * 2 + 0) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[2][tid]) : 0.0;
-        W.bandpeak[(j * 2 + 1) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[3][tid]) : 0.0;
+        K.smr[(j * 2 + 0) * PAC_NB + tid] = has ? pac_order_unkey(key[0][tid]) : -96.0;
+        K.smr[(j * 2 + 1) * PAC_NB + tid] = has ? pac_order_unkey(key[1][tid]) : -96.0;
+        K.bandpeak[(j * 2 + 0) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[2][tid]) : 0.0;
+        K.bandpeak[(j * 2 + 1) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[3][tid]) : 0.0;
     }
 }
 
@@ -337,25 +354,24 @@ __device__ long bitalloc_master(const double* __restrict__ smr_g, const uint8_t*
 }
 
 // One wave per stream of the chunk: the serial reservoir chain over the
-// stream's blocks t0 .. t0+S-1, and the stream's running byte cursor (each
-// channel-block's staging offset, in file order).
+// stream's blocks t0 .. t0+S-1 and each channel-block's byte count.
 __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict__ T,
                                                     const PacHuffTables* __restrict__ H,
-                                                    PacMasterWork W, const int64_t* __restrict__ blk_off,
-                                                    PacMasterChunk ck, int64_t* __restrict__ st_extra,
-                                                    int64_t* __restrict__ st_deposit,
-                                                    int64_t* __restrict__ st_cursor,
-                                                    int64_t* __restrict__ off, double bitBudget) {
+                                                    PacMasterChunkBuf K, PacMasterFields F,
+                                                    const int64_t* __restrict__ blk_off, PacMasterChunk ck,
+                                                    int64_t* __restrict__ st_extra,
+                                                    int64_t* __restrict__ st_deposit, double bitBudget) {
     __shared__ int ba_s[PAC_NB], sf_s[PAC_NB];
     const int lane = threadIdx.x;
     const int sl = blockIdx.x;
     const int s = ck.s_first + sl;
-    const int64_t len = blk_off[s + 1] - blk_off[s];
+    const int64_t b0 = blk_off[s];
+    const int64_t len = blk_off[s + 1] - b0;
     const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
     long extra = st_extra[s], deposit = st_deposit[s];
-    int64_t cur = st_cursor[s];
     for (int64_t t = ck.t0; t < t_end; ++t) {
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
+        const int64_t gb = b0 + t;
         // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
         long e = 0;
         if (deposit > 10) { e = deposit / 100; deposit -= e; }
@@ -363,21 +379,21 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
         extra += e;
         long dep_add = 0;
         for (int ch = 0; ch < 2; ++ch) {
-            const int64_t g = j * 2 + ch;
+            const int64_t gl = j * 2 + ch, g = gb * 2 + ch;
             int ba;
-            const long diff = bitalloc_master(W.smr + g * PAC_NB, W.lrms + j * PAC_NB, T, bitBudget, extra, 16,
+            const long diff = bitalloc_master(K.smr + gl * PAC_NB, F.lrms + gb * PAC_NB, T, bitBudget, extra, 16,
                                               lane, &ba);
             extra += diff;
             if (lane < PAC_NB) {
                 ba_s[lane] = ba;
-                const int sf = pac_scale_factor(W.bandpeak[g * PAC_NB + lane], ba);
+                const int sf = pac_scale_factor(K.bandpeak[gl * PAC_NB + lane], ba);
                 sf_s[lane] = sf;
-                W.ba[g * PAC_NB + lane] = (uint8_t)ba;
-                W.sf[g * PAC_NB + lane] = (uint8_t)sf;
+                F.ba[g * PAC_NB + lane] = (uint8_t)ba;
+                F.sf[g * PAC_NB + lane] = (uint8_t)sf;
             }
             wave_sync();
             // StripSignBits + Huffman.encodeData scoring of the 10 tables
-            const double* ln = W.lines + g * PAC_HALFN;
+            const double* ln = K.lines + gl * PAC_HALFN;
             int acc[PAC_NTAB];
 #pragma unroll
             for (int tb = 0; tb < PAC_NTAB; ++tb) acc[tb] = 0;
@@ -407,18 +423,15 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
             }
             dep_add += (long)orig - ((long)best + nsign + 4);
             const int nbits = 8 + 8 * PAC_NB + nsign + best + PAC_NB;
-            const int nbytes = 4 + (nbits + 7) / 8;
             if (lane == 0) {
-                W.tid[g] = (uint8_t)bestid;
-                W.nbytes[g] = nbytes;
-                off[g] = cur;
+                F.tid[g] = (uint8_t)bestid;
+                F.nbytes[g] = 4 + (nbits + 7) / 8;
             }
-            cur += nbytes;
             wave_sync();
         }
         deposit += dep_add;     // depositBits per channel (codec.py:120)
     }
-    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; st_cursor[s] = cur; }
+    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
 }
 
 __device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
@@ -432,44 +445,44 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
     return x - v;
 }
 
-// One wave per channel-block g = 2*j + ch of the chunk.
-__global__ __launch_bounds__(64) void k_master_pack(const PacTables* __restrict__ T,
-                                                    const PacHuffTables* __restrict__ H,
-                                                    PacMasterWork W, const int64_t* __restrict__ blk_off,
-                                                    PacMasterChunk ck, const int64_t* __restrict__ off,
-                                                    uint8_t* __restrict__ stage) {
-    __shared__ uint32_t words[PACK_WORDS];
-    __shared__ int bas[PAC_NB], sfs[PAC_NB], bstart[PAC_NB + 1];
-    __shared__ int rowsum[16];
-    const int lane = threadIdx.x;
-    const int64_t g = blockIdx.x;
-    const int64_t j = g >> 1;
-    int64_t gb;
-    if (!chunk_block(blk_off, ck, j, &gb)) return;
+// PACFile.WriteDataBlock's packing of one master channel-block
+// (pacfile.py:288-351) by one wave: overall(4) tableID(4), per band
+// (ba?ba-1:0)(4) sf(4) [+ nLines sign bits + the Huffman codes], LRMS(25),
+// MSB-first into LDS words, then '<L nBytes' + payload to out (null: skip).
+__device__ void wave_pack_master(const PacTables* __restrict__ T, const PacHuffTables* __restrict__ H,
+                                 const PacMasterFields& F, int64_t g, int64_t gb, const double* ln,
+                                 uint32_t* words, int* bas, int* sfs, int* bstart, int* pre_at_lower, int lane,
+                                 uint8_t* __restrict__ out) {
     for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
     if (lane < PAC_NB) {
-        bas[lane] = W.ba[g * PAC_NB + lane];
-        sfs[lane] = W.sf[g * PAC_NB + lane];
+        bas[lane] = F.ba[g * PAC_NB + lane];
+        sfs[lane] = F.sf[g * PAC_NB + lane];
     }
     wave_sync();
-    const int tid = W.tid[g] - 1;
-    const double* ln = W.lines + g * PAC_HALFN;
+    const int tb = F.tid[g] - 1;
     // per line: sign + code of length clen (0 for ba == 0 bands)
     uint32_t code[16], sgn[16];
     int clen[16], esc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        int l = q * WAVE + lane;
-        int b = T->band_of_line[l];
-        int ba = bas[b];
+        const int l = q * WAVE + lane;
+        const int b = T->band_of_line[l];
+        const int ba = bas[b];
         clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
+        uint32_t m = 0;
         if (ba) {
-            uint32_t m = pac_mantissa(ln[l], sfs[b], ba);
-            uint32_t sym = m & ((1u << (ba - 1)) - 1u);
+            m = pac_mantissa(ln[l], sfs[b], ba);
+            const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
             sgn[q] = (m >> (ba - 1)) & 1u;
-            int L = H->len[tid][sym];
-            if (L) { clen[q] = L; code[q] = H->bits[tid][sym]; }
-            else { clen[q] = H->esc_len[tid] + ba; esc[q] = 1; code[q] = sym; }
+            const int L = H->len[tb][sym];
+            if (L) { clen[q] = L; code[q] = H->bits[tb][sym]; }
+            else { clen[q] = H->esc_len[tb] + ba; esc[q] = 1; code[q] = sym; }
+        }
+        if (F.dbg_code) {
+            const int64_t i = g * PAC_HALFN + l;
+            F.dbg_mant[i] = m;
+            F.dbg_code[i] = esc[q] ? (((uint64_t)H->esc_bits[tb] << ba) | code[q]) : (uint64_t)code[q];
+            F.dbg_len[i] = (uint8_t)clen[q];
         }
     }
     // exclusive prefix of code lengths in line order (row q holds lines 64q..64q+63)
@@ -478,71 +491,100 @@ __global__ __launch_bounds__(64) void k_master_pack(const PacTables* __restrict_
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         int tot;
-        int ex = wave_excl_scan_i(clen[q], lane, &tot);
+        const int ex = wave_excl_scan_i(clen[q], lane, &tot);
         pre[q] = run + ex;
         run += tot;
     }
-    // band starts: 8 + sum_{b'<b} (8 + [ba>0](nl + codebits_b'))
+    // band starts without code bits: 8 + sum_{b'<b} (8 + [ba>0] nl)
     if (lane == 0) {
         int p = 8;
         for (int b = 0; b < PAC_NB; ++b) { bstart[b] = p; p += 8; if (bas[b]) p += T->nlines[b]; }
         bstart[PAC_NB] = p;   // LRMS bits start (minus all code bits, added below)
     }
-    // code bits of all earlier bands: codebits before line lower[b] = pre at that line
-    __shared__ int pre_at_lower[PAC_NB];
+    // code bits of all earlier bands = the prefix at the band's first line
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        int l = q * WAVE + lane;
-        int b = T->band_of_line[l];
-        if (l == T->lower[b]) pre_at_lower[b] = pre[q];
+        const int l = q * WAVE + lane;
+        const int b = T->band_of_line[l];
+        if (l == T->lower[b] && T->nlines[b]) pre_at_lower[b] = pre[q];
     }
     wave_sync();
+    if (lane == 0)      // empty bands: the prefix of the next band (or all code bits)
+        for (int b = PAC_NB - 1; b >= 0; --b)
+            if (!T->nlines[b]) pre_at_lower[b] = b == PAC_NB - 1 ? run : pre_at_lower[b + 1];
+    wave_sync();
     if (lane == 0) {
-        put_bits(words, 0, (uint32_t)W.overall[g], 4);
-        put_bits(words, 4, (uint32_t)(tid + 1), 4);
+        put_bits(words, 0, (uint32_t)F.overall[g], 4);
+        put_bits(words, 4, (uint32_t)(tb + 1), 4);
     }
     if (lane < PAC_NB) {
-        int b = lane, ba = bas[b];
-        int p = bstart[b] + pre_at_lower[b];
+        const int b = lane, ba = bas[b];
+        const int p = bstart[b] + pre_at_lower[b];
         put_bits(words, p, (uint32_t)(ba ? ba - 1 : 0), 4);
         put_bits(words, p + 4, (uint32_t)sfs[b], 4);
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        int l = q * WAVE + lane;
-        int b = T->band_of_line[l];
-        int ba = bas[b];
+        const int l = q * WAVE + lane;
+        const int b = T->band_of_line[l];
+        const int ba = bas[b];
         if (!ba) continue;
-        int p0 = bstart[b] + pre_at_lower[b] + 8;
+        const int p0 = bstart[b] + pre_at_lower[b] + 8;
         put_bits(words, p0 + (l - T->lower[b]), sgn[q], 1);
-        int pc = p0 + T->nlines[b] + (pre[q] - pre_at_lower[b]);
+        const int pc = p0 + T->nlines[b] + (pre[q] - pre_at_lower[b]);
         if (esc[q]) {
-            int el = H->esc_len[tid];
-            put_bits(words, pc, H->esc_bits[tid], el);
+            const int el = H->esc_len[tb];
+            put_bits(words, pc, H->esc_bits[tb], el);
             put_bits(words, pc + el, code[q], ba);
         } else {
             put_bits(words, pc, code[q], clen[q]);
         }
     }
-    if (lane < PAC_NB) {
-        int p = bstart[PAC_NB] + run + lane;
-        put_bits(words, p, (uint32_t)W.lrms[j * PAC_NB + lane], 1);
-    }
+    if (lane < PAC_NB) put_bits(words, bstart[PAC_NB] + run + lane, (uint32_t)F.lrms[gb * PAC_NB + lane], 1);
     wave_sync();
-    const int nbytes = W.nbytes[g] - 4;
-    store_block_bytes(stage + off[g], words, nbytes, lane);
+    if (out) store_block_bytes(out, words, F.nbytes[g] - 4, lane);
 }
 
-// after a stream group: every stream's bytes from its staging area to its
-// final offset (one workgroup per stream)
-__global__ __launch_bounds__(256) void k_copy_streams(const uint8_t* __restrict__ stage,
-                                                      const int64_t* __restrict__ src_off,
-                                                      const int64_t* __restrict__ dst_off,
-                                                      const int64_t* __restrict__ size,
-                                                      uint8_t* __restrict__ out) {
-    const int s = blockIdx.x;
-    const uint8_t* a = stage + src_off[s];
-    uint8_t* b = out + dst_off[s];
-    const int64_t n = size[s];
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) b[i] = a[i];
+// Pass 2: one 256-thread workgroup per stereo block gb (XCD-aware order):
+// the block's MDCT lines are recomputed exactly as k_master_front computes
+// them (same kernels, same arithmetic: identical values), then waves 0 and 1
+// pack channels 0 and 1 at their final offsets.  A channel-block that would
+// end past cap is skipped; the host reports PAC_E_CAPACITY from the total.
+__global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTables* __restrict__ T,
+                                                     const PacHuffTables* __restrict__ H, PacMasterFields F,
+                                                     int64_t nblocks, const int64_t* __restrict__ off,
+                                                     uint8_t* __restrict__ out, int64_t cap) {
+    __shared__ double2 bufA[1024], bufB[1024];     // 32 KB: MDCT L / R, then the coded lines
+    __shared__ uint32_t words[2][PACK_WORDS];
+    __shared__ int bas[2][PAC_NB], sfs[2][PAC_NB], bstart[2][PAC_NB + 1], pal[2][PAC_NB];
+    __shared__ uint8_t lr[PAC_NB];
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int w = tid / WAVE;
+    const int64_t gb = xcd_item(blockIdx.x, nblocks);
+    const BlockPcm rL(locate(src, gb, 0));
+    const BlockPcm rR(locate(src, gb, 1));
+    if (tid < PAC_NB) lr[tid] = F.lrms[gb * PAC_NB + tid];
+    const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
+    const double* XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
+    const double gL = (double)(1 << F.overall[gb * 2]), gR = (double)(1 << F.overall[gb * 2 + 1]);
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    double* L0 = reinterpret_cast<double*>(bufA);
+    double* L1 = reinterpret_cast<double*>(bufB);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {     // each line is read and rewritten by its own thread
+        const int l = i * 256 + tid;
+        const double xl = __dmul_rn(XL[l], gL), xr = __dmul_rn(XR[l], gR);
+        const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
+        const int ms = l < lend ? lr[T->band_of_line[l]] : 0;
+        L0[l] = ms ? M : xl;
+        L1[l] = ms ? S : xr;
+    }
+    __syncthreads();
+    if (w < 2) {
+        const int64_t g = gb * 2 + w;
+        const int nb = F.nbytes[g];
+        uint8_t* o = (off[g] + nb <= cap) ? out + off[g] : nullptr;
+        wave_pack_master(T, H, F, g, gb, w ? L1 : L0, words[w], bas[w], sfs[w], bstart[w], pal[w], lane, o);
+    }
 }

@@ -31,4 +31,9 @@ def ctx():
 
 
 def fixture(name):
+    """A committed reference fixture (tests/fixtures/MANIFEST.json): inputs/*.wav
+    are the reference's inputs/*.wav, coded/ its verified .pac/.wak files."""
+    for d in (FIX, os.path.join(FIX, "inputs"), os.path.join(FIX, "coded")):
+        if os.path.exists(os.path.join(d, name)):
+            return os.path.join(d, name)
     return os.path.join(FIX, name)

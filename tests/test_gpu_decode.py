@@ -25,7 +25,7 @@ def sha(b):
 
 
 def _path(name):
-    return os.path.join(ROOT, "tests", name) if name.startswith("fixtures/") else os.path.join(GOLD, name)
+    return fixture(name[len("fixtures/"):]) if name.startswith("fixtures/") else os.path.join(GOLD, name)
 
 
 @pytest.mark.parametrize("name", sorted(MAN["shim"]))

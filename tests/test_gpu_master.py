@@ -137,3 +137,99 @@ def test_codec_encode_tuple_master(ctx):
         assert tid[c] == ob.table_id[c]
         assert list(ba[c]) == list(ob.ba[c])
         assert list(sf[c]) == list(ob.sf[c])
+        nl = cp.sfBands.nLines
+        bal = np.repeat(np.array(ob.ba[c][:]), nl)
+        om = np.array(ob.mant[c][:])[:len(bal)]
+        keep = bal > 0
+        assert signs[c] == [int(m >> (b - 1)) & 1 for m, b in zip(om[keep], bal[keep])]
+        assert len(codes[c]) == int(keep.sum()) and all(isinstance(s, str) and s for s in codes[c])
+
+
+class _Bits:
+    """MSB-first bit writer with PackedBits.WriteBits semantics (bitpack.py:36-101)."""
+
+    def __init__(self, nbytes):
+        self.b = bytearray(nbytes)
+        self.pos = 0
+
+    def write(self, value, n):
+        for i in range(n - 1, -1, -1):
+            if (value >> i) & 1:
+                self.b[self.pos >> 3] |= 0x80 >> (self.pos & 7)
+            self.pos += 1
+
+
+def _write_data_block_ref(tup, cp):
+    """Restatement of the reference's PACFile.WriteDataBlock packing loop
+    (codec/pacfile.py:288-351) consuming the codec.Encode 7-tuple exactly as
+    the reference does: len() and int(s, 2) of the Huffman code strings."""
+    import struct
+    scaleFactor, bitAlloc, signBits, mantissa, tableID, overallScaleFactor, LRMS = tup
+    out = b""
+    nl = cp.sfBands.nLines
+    for iCh in range(cp.nChannels):
+        nBits = cp.nScaleBits + cp.nTableIDBits
+        iMant = 0
+        for iBand in range(cp.sfBands.nBands):
+            nBits += cp.nMantSizeBits + cp.nScaleBits
+            if bitAlloc[iCh][iBand]:
+                nBits += nl[iBand]
+                for j in range(nl[iBand]):
+                    nBits += len(mantissa[iCh][iMant + j])
+                iMant += nl[iBand]
+        nBits += len(LRMS)
+        nBytes = nBits // 8 + (1 if nBits % 8 else 0)
+        out += struct.pack("<L", nBytes)
+        pb = _Bits(nBytes)
+        pb.write(overallScaleFactor[iCh], cp.nScaleBits)
+        pb.write(tableID[iCh], cp.nTableIDBits)
+        iMant = 0
+        for iBand in range(cp.sfBands.nBands):
+            ba = bitAlloc[iCh][iBand]
+            pb.write(ba - 1 if ba else 0, cp.nMantSizeBits)
+            pb.write(int(scaleFactor[iCh][iBand]), cp.nScaleBits)
+            if bitAlloc[iCh][iBand]:
+                for j in range(nl[iBand]):
+                    pb.write(signBits[iCh][iMant + j], 1)
+                for j in range(nl[iBand]):
+                    s = mantissa[iCh][iMant + j]
+                    pb.write(int(s, 2), len(s))
+                iMant += nl[iBand]
+        for iBand in range(cp.sfBands.nBands):
+            pb.write(int(LRMS[iBand]), 1)
+        out += bytes(pb.b)
+    return out
+
+
+def test_codec_encode_tuple_feeds_reference_writer(ctx):
+    """The master codec.Encode tuple (signBits, Huffman code strings, tableID,
+    ...) consumed by a restatement of the reference's WriteDataBlock packing
+    loop reproduces coded/piano_test2.wak block by block (first 40 blocks)."""
+    from pac_amd import codec
+    from pac_amd.huffman import Huffman
+    from pac_amd.pcmfile import PCMFile
+    from pac_amd.psychoac import ScaleFactorBands, AssignMDCTLinesFromFreqLimits
+    with open(fixture("piano_test2.wak"), "rb") as f:
+        ref = f.read()
+    fs, nch, ns, nlines, off = P.parse_pac_header(ref)
+    inFile = PCMFile(fixture("piano_test2.wav"))
+    cp = inFile.OpenForReading()
+    cp.nMDCTLines = cp.nSamplesPerBlock = 1024
+    cp.nScaleBits, cp.nMantSizeBits, cp.targetBitsPerSample, cp.nTableIDBits = 4, 4, 2.27, 4
+    cp.sfBands = ScaleFactorBands(AssignMDCTLinesFromFreqLimits(1024, cp.sampleRate))
+    cp.extraBits = 0
+    h = Huffman()
+    prior = [np.zeros(1024) for _ in range(nch)]
+    pos = off
+    for blk in range(40):
+        data = inFile.ReadDataBlock(cp)
+        if data is None:
+            break
+        full = [np.concatenate((prior[c], data[c])) for c in range(nch)]
+        prior = data
+        tup = codec.Encode(full, cp, h, profile=codec.PROFILE_MASTER, context=ctx)
+        assert all(isinstance(s, str) for s in tup[3][0])
+        got = _write_data_block_ref(tup, cp)
+        assert got == ref[pos:pos + len(got)], "block %d differs" % blk
+        pos += len(got)
+    inFile.Close(cp)

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, REF, fixture
+from conftest import FIX, GOLD, REF, fixture
 
 import pyoracle as P
 from pac_amd.pcmfile import codes_to_float
@@ -130,27 +130,42 @@ def test_zero_block_mdct_signs_match_reference():
     assert np.array_equal(np.signbit(X), neg)
 
 
-REF_FIXTURES = [("inputs/harpsichord.wav", "coded/harpsichord.pac", P.ORIGIN),
-                ("PerceptualAudioCodec_Origin/inputs/german.wav", "coded/german.pac", P.ORIGIN),
-                ("PerceptualAudioCodec_Origin/inputs/trumpet.wav", "coded/trumpet.pac", P.ORIGIN)] + [
-    ("inputs/%s.wav" % n, "coded/%s.wak" % n, P.MASTER) for n in
+# Every verified reference bitstream, committed under
+# tests/fixtures/ (MANIFEST.json): (input wav, coded file, profile)
+REF_FIXTURES = [("harpsichord.wav", "harpsichord.pac", P.ORIGIN),
+                ("german.wav", "german.pac", P.ORIGIN),
+                ("trumpet.wav", "trumpet.pac", P.ORIGIN)] + [
+    ("%s.wav" % n, "%s.wak" % n, P.MASTER) for n in
     ("piano_test2 harmonic_test2 harmonic_test4 percussion_test1 percussion_test2 "
      "percussion_test3 piano_test3 pop_test2 rock rock_test2 speech_test2 speech_test3").split()] + [
-    ("inputs/speech_test3.wav", "coded/withHuffman/speech_test3.wak", P.MASTER)]
+    ("speech_test3.wav", "withHuffman/speech_test3.wak", P.MASTER)]
 
 
-@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
 @pytest.mark.parametrize("inp,coded,prof", REF_FIXTURES, ids=[c for _, c, _ in REF_FIXTURES])
 def test_reference_fixture_prefix(inp, coded, prof):
-    """Every verified reference bitstream: the first 48
-    blocks byte for byte (the encoder is causal, so a prefix is a full check
-    of those blocks incl. the reservoir chain)."""
-    fs, nch, n, pcm = P.read_wav(os.path.join(REF, inp))
+    """Every verified reference bitstream: the first 48 blocks byte for byte
+    (the encoder is causal, so a prefix is a full check of those blocks incl.
+    the reservoir chain; the GPU tests check the whole files)."""
+    fs, nch, n, pcm = P.read_wav(fixture(inp))
     o = P.Oracle(fs, huffman=(prof == P.MASTER))
     got = P.pac_header(fs, nch, n, o.nlines()) + o.encode_data(prof, pcm, max_blocks=48)
-    with open(os.path.join(REF, coded), "rb") as f:
+    with open(fixture(coded), "rb") as f:
         ref = f.read()
     assert got == ref[:len(got)]
+
+
+def test_fixture_manifest():
+    """The committed reference fixtures are the reference's files, unchanged."""
+    import hashlib
+    with open(os.path.join(FIX, "MANIFEST.json")) as f:
+        m = json.load(f)
+    assert len(m["files"]) == 38
+    for rel, e in m["files"].items():
+        with open(os.path.join(FIX, rel), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == e["sha256"], rel
+        if os.path.isdir(REF):
+            with open(os.path.join(REF, e["reference"]), "rb") as f:
+                assert hashlib.sha256(f.read()).hexdigest() == e["sha256"], rel
 
 
 def test_manifest_hashes():

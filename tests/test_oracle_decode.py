@@ -15,7 +15,7 @@ import os
 
 import pytest
 
-from conftest import GOLD, REF, ROOT
+from conftest import fixture, GOLD, REF, ROOT
 
 import pyoracle as P
 
@@ -28,20 +28,20 @@ def sha(b):
 
 @pytest.mark.parametrize("name", sorted(MAN["shim"]))
 def test_decode_equals_reference_shim(name):
-    path = os.path.join(ROOT, "tests", name) if name.startswith("fixtures/") else os.path.join(GOLD, name)
+    path = fixture(name[len("fixtures/"):]) if name.startswith("fixtures/") else os.path.join(GOLD, name)
     prof = P.ORIGIN if name.endswith(".pac") else P.MASTER
     assert sha(P.decode_file(path, prof)) == MAN["shim"][name]["sha256"]
 
 
 def test_piano_test2_decode_equals_reference_output():
-    got = P.decode_file(os.path.join(ROOT, "tests", "fixtures", "piano_test2.wak"), P.MASTER)
+    got = P.decode_file(fixture("piano_test2.wak"), P.MASTER)
     assert sha(got) == MAN["reference_outputs"]["piano_test2"]
 
 
-@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
 @pytest.mark.parametrize("name", sorted(MAN["reference_outputs"]))
 def test_decode_equals_reference_outputs(name):
-    got = P.decode_file(os.path.join(REF, "coded", name + ".wak"), P.MASTER)
+    """the reference's own decodes outputs/<name>.wav (sha256) of the committed .wak"""
+    got = P.decode_file(fixture(name + ".wak"), P.MASTER)
     assert sha(got) == MAN["reference_outputs"][name]
     with open(os.path.join(REF, "outputs", name + ".wav"), "rb") as f:
         assert got == f.read()

@@ -182,6 +182,14 @@ static void build_tables(int fs, PacTables* t) {
         if (v > mx) mx = v;
     }
     for (int k = 0; k < PAC_HALFN; k++) t->mld[k] = t->mld[k] / mx;
+    {
+        const long double kl = (long double)(-27.0 * 0.33219280948873624);   // PAC_KL, double-rounded
+        for (int l = 0; l < PAC_HALFN; l++) {
+            const long double e = kl * (long double)t->bark_line[l];
+            t->pow_kl[l] = (double)exp2l(e);
+            t->pow_mkl[l] = (double)exp2l(-e);
+        }
+    }
     for (int l = 0, ku = 0, kv = 0; l < PAC_HALFN; l++) {   // bark_line ascending in l
         const double zl = t->bark_line[l];
         while (ku < PAC_HALFN - 1 && zl - t->bark_bin[ku] > 0.5) ku++;
@@ -533,6 +541,29 @@ static int report_phase_clocks(pac_ctx* c, hipStream_t s, int64_t n) {
     return PAC_OK;
 }
 
+// diagnostic build (-DPAC_ROWPROF): masking-row statistics of the last call
+static int report_rowprof(pac_ctx* c, hipStream_t s) {
+#ifdef PAC_ROWPROF
+    std::vector<unsigned long long> all(1024 * 16);
+    unsigned long long rp[16] = {0};
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(pac_rowprof), all.size() * 8));
+    for (int i = 0; i < 1024 * 16; i++) rp[i % 16] += all[i];
+    const double n = (double)(rp[0] ? rp[0] : 1);
+    fprintf(stderr, "ROWPROF rows %llu  cyc lower %.0f flat %.0f skip %.0f mom %.0f direct+rag %.0f | nm %.1f "
+            "momrows %.3f D %.2f mom_n %.1f rag %.1f flatlen %.1f lowlen %.1f m0 %.1f direct_n %.1f\n",
+            rp[0], rp[1] / n, rp[2] / n, rp[3] / n, rp[4] / n, rp[5] / n, rp[6] / n, rp[7] / n,
+            rp[8] / (double)(rp[7] ? rp[7] : 1), rp[9] / n, rp[10] / n, rp[11] / n, rp[12] / n, rp[13] / n,
+            rp[14] / n);
+    std::fill(all.begin(), all.end(), 0ull);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pac_rowprof), all.data(), all.size() * 8));
+#else
+    (void)c;
+    (void)s;
+#endif
+    return PAC_OK;
+}
+
 static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src, int64_t G,
                       uint8_t* out_dev, int64_t out_cap, int64_t* out_total, int64_t** off_dev) {
     int rc;
@@ -553,23 +584,6 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     hipLaunchKernelGGL(k_origin_front, dim3((unsigned)G), dim3(FRONT_NT), 0, s, src, T, W, G);
     HIPCHK(hipGetLastError());
     if (c->dbg & 16) report_phase_clocks(c, s, nprof);
-#ifdef PAC_ROWPROF
-    {
-        std::vector<unsigned long long> all(1024 * 16);
-        unsigned long long rp[16] = {0};
-        HIPCHK(hipStreamSynchronize(s));
-        HIPCHK(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(pac_rowprof), all.size() * 8));
-        for (int i = 0; i < 1024 * 16; i++) rp[i % 16] += all[i];
-        const double n = (double)(rp[0] ? rp[0] : 1);
-        fprintf(stderr, "ROWPROF rows %llu  cyc lower %.0f flat %.0f skip %.0f mom %.0f direct+rag %.0f | nm %.1f "
-                "momrows %.3f D %.2f mom_n %.1f rag %.1f flatlen %.1f lowlen %.1f m0 %.1f direct_n %.1f\n",
-                rp[0], rp[1] / n, rp[2] / n, rp[3] / n, rp[4] / n, rp[5] / n, rp[6] / n, rp[7] / n,
-                rp[8] / (double)(rp[7] ? rp[7] : 1), rp[9] / n, rp[10] / n, rp[11] / n, rp[12] / n, rp[13] / n,
-                rp[14] / n);
-        std::fill(all.begin(), all.end(), 0ull);
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pac_rowprof), all.data(), all.size() * 8));
-    }
-#endif
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_origin_alloc, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, T, W, G,
                        bit_budget(p), 16);
@@ -822,7 +836,7 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         HIPCHK(hipStreamSynchronize(s));
     }
     if (!master) finish_timing(c, G, total);
-    return PAC_OK;
+    return report_rowprof(c, s);
 }
 
 // --- per-block API ----------------------------------------------------------

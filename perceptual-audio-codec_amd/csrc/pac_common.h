@@ -53,6 +53,9 @@ struct PacTables {
     // exact double comparisons, fl(z_l - z) is monotone in z.  With the rank
     // of each bin among the maskers this gives the zone bounds U, V per line.
     int16_t mask_ku[PAC_HALFN], mask_kv[PAC_HALFN];
+    // factored masking sums (pac_wave.h): 2^(KL z_l) and 2^(-KL z_l) per line,
+    // KL = -27 log2(10)/10 as the device rounds it, evaluated in long double
+    double pow_kl[PAC_HALFN], pow_mkl[PAC_HALFN];
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

@@ -168,10 +168,9 @@ __device__ __forceinline__ double pac_order_unkey(unsigned long long k) {
 __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, const PacTables* __restrict__ T,
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
-    __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then per-wave beta rows
+    __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then the loud masker list
     __shared__ int16_t rank[PAC_HALFN];   // 2 KB: masker rank of each bin (4 workgroups per CU)
     // the small reduction scratch lives in whichever region is idle at that point
-    int* cnt = reinterpret_cast<int*>(xs);         // free once the spectrum input is staged
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
@@ -215,13 +214,14 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
     grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf,
                                reinterpret_cast<double2*>(xs), tid);
     PROF_MARK(4);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, cnt, rank);
+    const MaskerLists L = masker_lists(buf, xs, rank);
+    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, L);
     PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     // Masking rows are claimed dynamically, most expensive first (the order
     // measured on broadband input: middle rows carry the most maskers on both
     // sides); a wave keeps its (row, threshold) pairs in registers, at most 4.
-    int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));   // slot the list never uses
+    int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
     __syncthreads();
     double tv0 = 0.0, tv1 = 0.0, tv2 = 0.0, tv3 = 0.0;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
-        const double thr = wave_masking_row(buf, nm, T, lane, r, xs + w * 512, rank);
+        const double thr = wave_masking_row(L, nm, T, lane, r);
         switch (nr) {
             case 0: tv0 = thr; break;
             case 1: tv1 = thr; break;
@@ -500,16 +500,15 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
                                                         int32_t* __restrict__ npeaks) {
     __shared__ double2 buf[1024];
     __shared__ double2 tmp[1024];
-    __shared__ double beta[512];
+    __shared__ int16_t rank[PAC_HALFN];
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
     wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
-    int16_t* rank = reinterpret_cast<int16_t*>(tmp + 512);   // past the peak scratch
-    int nm = wave_find_maskers(buf, T, no_drop ? 0.0 : 15.0, lane, reinterpret_cast<int*>(tmp), rank);
-    double thr[16];
-    wave_masking(buf, nm, T, lane, thr, beta, rank);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = thr[q];
+    const MaskerLists L = masker_lists(buf, tmp, rank);
+    const int nm = grp_find_maskers<WAVE>(buf, T, no_drop ? 0.0 : 15.0, lane, L);
+#pragma unroll 1
+    for (int q = 0; q < 16; ++q)
+        thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = wave_masking_row(L, nm, T, lane, q);
     if (lane == 0) npeaks[blockIdx.x] = nm;
 }
 

@@ -85,12 +85,11 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
                                                          PacMasterChunkBuf K, PacMasterChunk ck) {
-    __shared__ double2 buf[1024];
-    __shared__ __attribute__((aligned(16))) double beta[4 * 512];   // FFT / peak scratch, then beta rows
+    __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
+    __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // FFT scratch, then loud list (region B)
     __shared__ int16_t rank[PAC_HALFN];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
-    const int w = tid / WAVE;
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
     const int64_t j = item / 6;                // block within the chunk
     const int v = (int)(item % 6);
@@ -99,11 +98,12 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
-    grp_spectrum_pow<FRONT_NT>(d, T, buf, reinterpret_cast<double2*>(beta), tid);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, reinterpret_cast<int*>(beta), rank);
+    grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
+    const MaskerLists L = masker_lists(buf, tmp, rank);
+    const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     // rows claimed dynamically, most expensive first (as in k_origin_front)
-    int* rowctr = reinterpret_cast<int*>(mk_E(buf) + (PAC_MAXMASK - 1));
+    int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
     __syncthreads();
 #pragma unroll 1
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
-        out[r * WAVE + lane] = wave_masking_row(buf, nm, T, lane, r, beta + w * 512, rank);
+        out[r * WAVE + lane] = wave_masking_row(L, nm, T, lane, r);
     }
 }
 

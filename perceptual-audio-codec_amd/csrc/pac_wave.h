@@ -271,43 +271,177 @@ __device__ __forceinline__ void wave_spectrum_pow(const DS& d, const PacTables* 
     grp_spectrum_pow<WAVE>(d, T, buf, tmp, lane);
 }
 
-// Masker list in LDS, structure of arrays over the 16 KB scratch (2048 doubles):
-//   z[m]   Bark(f_m)                                       [0, 512)
-//   B[m]   (SPL_m - drop - 96) * log2(10)/10               [512, 1024)
-//   ku[m]  (0.367*max(SPL_m-40,0) - 27) * log2(10)/10      [1024, 1536)
-//   E[m]   2^B[m] = 10^((SPL_m - drop - 96)/10)            [1536, 2048)
-// Maskers are in ascending frequency, the reference's summation order.
+// ---------------------------------------------------------------------------
+// masking threshold (psychoac.py:409-456)
+// ---------------------------------------------------------------------------
+//
+// Per MDCT line l the reference adds, in ascending masker order from 0,
+//   10^((SPL_m + spread_m(dz) - drop - 96) / 10),   dz = Bark(f_l) - Bark(f_m),
+// spread (psychoac.py:111-116) = (0.367 max(SPL_m - 40, 0) [dz >= 0] - 27) (|dz| - 1/2) for |dz| > 1/2.
+// In base 2 with B_m = (SPL_m - drop - 96) log2(10)/10 and the slopes
+// KL = -27 log2(10)/10 (line below the masker), ku_m = (0.367 max(SPL_m-40,0) - 27) log2(10)/10
+// (line above it), the maskers of line l split into three zones by the rank
+// bounds U(l) = #{m : dz > 1/2}, V(l) = #{m : dz >= -1/2} (maskers are in
+// ascending frequency):
+//   flat   U <= m < V:  E_m = 2^B_m                 -> dd prefix sums, one difference per line
+//   lower  m >= V:      2^(B_m + KL (z_m - 1/2)) * 2^(-KL z_l)   -> one suffix sum per threshold
+//   upper  m < U:       2^(B_m + ku_m (z_l - z_m - 1/2))
+//     quiet maskers (SPL_m <= 40: ku_m = KL exactly) factor the same way:
+//                       2^(B_m - KL (z_m + 1/2)) * 2^(KL z_l)     -> one prefix sum per threshold
+//     loud maskers (the rest) keep their own slopes: per 64-line row, a Taylor
+//     series in the slope spread ("moment form") or the direct sum, over the
+//     compacted list of loud maskers only.
+// All terms are positive, so every regrouping above changes the result by a
+// few ulp at most (no cancellation); exponents are evaluated in double-double.
 #define PAC_LOG2_10_OVER_10 0.33219280948873624   // log2(10)/10
-#define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope (dz < 0), psychoac.py:116
+#define PAC_KL (-27.0 * PAC_LOG2_10_OVER_10)       // lower slope, and the slope of quiet maskers
 #define PAC_LN2 0.6931471805599453
 // order in which the 16 masking rows (64 lines each) are claimed by the waves
 // of a threshold kernel, 4 bits per row, most expensive first (measured on
 // broadband input: the middle rows carry the most maskers on both sides)
 #define PAC_ROW_ORDER 0xf0e1dc4528b9a763ull
-#define PAC_MOM_MIN 24      // fewest common upper maskers for the moment form
+#define PAC_MOM_MIN 24      // fewest common loud maskers for the moment form
 #define PAC_MOM_DMAX 40     // highest Taylor degree of the moment form
+#define PAC_MOM_K 4         // maskers per lane held in registers by the moment form (per group)
 
-__device__ __forceinline__ double* mk_z(double2* buf) { return reinterpret_cast<double*>(buf); }
-__device__ __forceinline__ double* mk_B(double2* buf) { return reinterpret_cast<double*>(buf) + 512; }
-__device__ __forceinline__ double* mk_ku(double2* buf) { return reinterpret_cast<double*>(buf) + 1024; }
-__device__ __forceinline__ double* mk_E(double2* buf) { return reinterpret_cast<double*>(buf) + 1536; }
+// 2^(h + l) for a double-double exponent (|l| << ulp(h)): exp2(h) * (1 + l ln2)
+__device__ __forceinline__ double pac_exp2_dd(double h, double l) {
+    return pac_exp2(h) * __builtin_fma(l, PAC_LN2, 1.0);
+}
+
+// c + k * (a - b) as a double-double (TwoSum, TwoProduct via fma, TwoSum)
+__device__ __forceinline__ void dd_affine(double c, double k, double a, double b, double& hi, double& lo) {
+    double s = a - b;
+    double bb = s - a;
+    double err = (a - (s - bb)) + (-b - bb);
+    double ph = k * s;
+    double pl = __builtin_fma(k, s, -ph) + k * err;
+    double t = c + ph;
+    double cc = t - c;
+    double e2 = (c - (t - cc)) + (ph - cc);
+    hi = t;
+    lo = e2 + pl;
+}
+
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+// (ah + al) + (bh + bl), renormalised
+__device__ __forceinline__ void dd_add(double ah, double al, double bh, double bl, double& h, double& l) {
+    double s, e;
+    two_sum(ah, bh, s, e);
+    e += al + bl;
+    h = s + e;
+    l = e - (h - s);
+}
+
+// The per-threshold masker lists in LDS.  Region A (16 KB, the spectrum's
+// buffer once the maskers are extracted): four arrays of 512 doubles indexed
+// by masker rank m = 0..nm (nm <= 511):
+//   pfh/pfl  exclusive dd prefix of E_m            (flat zone)
+//   sl       suffix sum from m of 2^(B + KL(z - 1/2))   (lower side; sl[nm] = 0)
+//   su       exclusive prefix of 2^(B - KL(z + 1/2)) over quiet maskers (upper side)
+// Region B (16 KB, the FFT scratch): the loud maskers' z, B, ku (12 KB), lpre
+// [m] = #loud maskers of rank < m, a few counters and the peak-compaction
+// scratch.  rank[k] (k < 1024) = #maskers with bin < k.
+struct MaskerLists {
+    double *pfh, *pfl, *sl, *su;
+    double *lz, *lB, *lku;
+    int16_t* lpre;
+    int* misc;       // [0] row counter of the claiming loop, [1] loud count
+    int* cnt;        // 32 ints: ballot segment counts
+    int* kidx;       // 512 ints: compacted peak bins
+    int16_t* rank;
+};
+__device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB, int16_t* rank) {
+    MaskerLists L;
+    double* a = reinterpret_cast<double*>(regA);
+    L.pfh = a;
+    L.pfl = a + 512;
+    L.sl = a + 1024;
+    L.su = a + 1536;
+    char* b = reinterpret_cast<char*>(regB);
+    L.lz = reinterpret_cast<double*>(b);
+    L.lB = reinterpret_cast<double*>(b + 4096);
+    L.lku = reinterpret_cast<double*>(b + 8192);
+    L.lpre = reinterpret_cast<int16_t*>(b + 12288);
+    L.misc = reinterpret_cast<int*>(b + 13312);
+    L.cnt = reinterpret_cast<int*>(b + 13312 + 64);
+    L.kidx = reinterpret_cast<int*>(b + 14336);
+    L.rank = rank;
+    return L;
+}
+
+// exclusive prefix (dd) of h[0..n) in place into (h, l)[0..n], by one wave
+__device__ __forceinline__ void wave_scan_excl_dd(double* h, double* l, int n, int lane) {
+    double ch = 0.0, cl = 0.0;
+    for (int base = 0; base <= n; base += WAVE) {
+        const int m = base + lane;
+        double xh = m < n ? h[m] : 0.0, xl = 0.0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double yh = __shfl_up(xh, o, WAVE), yl = __shfl_up(xl, o, WAVE);
+            if (lane >= o) dd_add(yh, yl, xh, xl, xh, xl);
+        }
+        const double th = __shfl(xh, 63, WAVE), tl = __shfl(xl, 63, WAVE);
+        double eh = __shfl_up(xh, 1, WAVE), el = __shfl_up(xl, 1, WAVE);
+        if (lane == 0) { eh = 0.0; el = 0.0; }
+        double rh, rl;
+        dd_add(ch, cl, eh, el, rh, rl);
+        if (m <= n) { h[m] = rh; l[m] = rl; }
+        dd_add(ch, cl, th, tl, ch, cl);
+    }
+}
+// exclusive prefix of x[0..n) in place into x[0..n], by one wave
+__device__ __forceinline__ void wave_scan_excl(double* x, int n, int lane) {
+    double carry = 0.0;
+    for (int base = 0; base <= n; base += WAVE) {
+        const int m = base + lane;
+        double v = m < n ? x[m] : 0.0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(v, o, WAVE);
+            if (lane >= o) v += y;
+        }
+        const double t = __shfl(v, 63, WAVE);
+        double e = __shfl_up(v, 1, WAVE);
+        if (lane == 0) e = 0.0;
+        if (m <= n) x[m] = carry + e;
+        carry += t;
+    }
+}
+// suffix sums x[m] = sum_{k >= m} x_k in place, x[n] = 0, by one wave
+__device__ __forceinline__ void wave_scan_suffix(double* x, int n, int lane) {
+    double carry = 0.0;
+    for (int base = (n / WAVE) * WAVE; base >= 0; base -= WAVE) {
+        const int m = base + lane;
+        double v = m < n ? x[m] : 0.0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_down(v, o, WAVE);
+            if (lane + o < 64) v += y;
+        }
+        const double t = __shfl(v, 0, WAVE);
+        if (m <= n) x[m] = carry + v;
+        carry += t;
+    }
+}
 
 // findpeaks (psychoac.py:158-191) on |X|^2 held in buf[k].x (the floor
 // 10 log10|X| > -30 is the equivalent |X|^2 > T->peak_floor2), masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
-// compacted masker list (ascending bin order) written over buf by a group of
-// NT threads.  scratch: LDS of 16 + 512 ints.  Returns the masker count.
-// Peaks are compacted first (ballots, bin order = the reference's summation
-// order) so that the SPL (a log10 each) is evaluated once per masker.
-// rank[k] (k < 1024) = #maskers with bin < k, for the zone bounds of the
-// masking sum (PacTables::mask_ku / mask_kv).
+// masker lists (MaskerLists) built by a group of NT threads.  Peaks are
+// compacted first (ballots, bin order = the reference's summation order) so
+// that the SPL (a log10 each) is evaluated once per masker.  Returns nm.
 template <int NT>
-__device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                double drop, int tid, int* scratch, int16_t* rank) {
+__device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T, double drop,
+                                                int tid, const MaskerLists& L) {
     constexpr int J = 1024 / NT;
     constexpr int NW = NT / WAVE;
-    int* cnt = scratch;              // [J][NW] peak counts of the (j, wave) segments, in bin order
-    int* kidx = scratch + 16;        // compacted peak bins
+    int* cnt = L.cnt;                // [J][NW] peak counts of the (j, wave) segments, in bin order
+    int* kidx = L.kidx;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
     const double floor2 = T->peak_floor2;
@@ -332,16 +466,20 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int idx = pre[j * NW + w] + __popcll(bal[j] & below);
-        rank[j * NT + tid] = (int16_t)idx;
+        L.rank[j * NT + tid] = (int16_t)idx;
         if ((bal[j] >> lane) & 1ull) kidx[idx] = j * NT + tid;
     }
     grp_sync<NT>();
     tot = __builtin_amdgcn_readfirstlane(tot);
     constexpr int R = (PAC_MAXMASK + NT - 1) / NT;
-    double rz[R], rB[R], rku[R], rE[R];
+    double rz[R], rB[R], rku[R], rE[R], rPL[R], rPU[R];
+    unsigned long long lb[R];
+    int* cnt2 = cnt + 16;            // [R][NW] loud counts
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int idx = q * NT + tid;
+        bool loud = false;
+        rz[q] = rB[q] = rku[q] = rE[q] = rPL[q] = rPU[q] = 0.0;
         if (idx < tot) {
             const int k = kidx[idx];
             double s = 0.0;
@@ -353,48 +491,52 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
             const double sp = pac_spl(csp * s);
             double lev = sp - 40.0;
             lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
+            loud = lev != 0.0;                            // else ku == KL exactly
             rB[q] = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
             rz[q] = T->bark_bin[k];
             rku[q] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
             rE[q] = pac_exp2(rB[q]);
+            double h, lo;
+            dd_affine(rB[q], PAC_KL, rz[q], 0.5, h, lo);       // B + KL (z - 1/2)
+            rPL[q] = pac_exp2_dd(h, lo);
+            if (!loud) {
+                dd_affine(rB[q], PAC_KL, -0.5, rz[q], h, lo);  // B - KL (z + 1/2)
+                rPU[q] = pac_exp2_dd(h, lo);
+            }
         }
+        lb[q] = __ballot(loud);
+        if (lane == 0) cnt2[q * NW + w] = __popcll(lb[q]);
     }
-    grp_sync<NT>();   // every |X|^2 read done before the list overwrites buf
-    double* mz = mk_z(buf);
-    double* mB = mk_B(buf);
-    double* mku = mk_ku(buf);
-    double* mE = mk_E(buf);
+    grp_sync<NT>();   // every |X|^2 read done before the lists overwrite buf; loud counts visible
+    int pre2[R * NW];
+    int nloud = 0;
+#pragma unroll
+    for (int i = 0; i < R * NW; ++i) { pre2[i] = nloud; nloud += cnt2[i]; }
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int idx = q * NT + tid;
-        if (idx < tot) { mz[idx] = rz[q]; mB[idx] = rB[q]; mku[idx] = rku[q]; mE[idx] = rE[q]; }
+        if (idx < tot) {
+            L.pfh[idx] = rE[q];
+            L.sl[idx] = rPL[q];
+            L.su[idx] = rPU[q];
+            const int j = pre2[q * NW + w] + __popcll(lb[q] & below);
+            L.lpre[idx] = (int16_t)j;
+            if ((lb[q] >> lane) & 1ull) { L.lz[j] = rz[q]; L.lB[j] = rB[q]; L.lku[j] = rku[q]; }
+        }
+    }
+    if (tid == 0) { L.lpre[tot] = (int16_t)nloud; L.misc[1] = nloud; }
+    grp_sync<NT>();
+    if constexpr (NW >= 3) {
+        if (w == 0) wave_scan_excl_dd(L.pfh, L.pfl, tot, lane);
+        else if (w == 1) wave_scan_suffix(L.sl, tot, lane);
+        else if (w == 2) wave_scan_excl(L.su, tot, lane);
+    } else {
+        wave_scan_excl_dd(L.pfh, L.pfl, tot, lane);
+        wave_scan_suffix(L.sl, tot, lane);
+        wave_scan_excl(L.su, tot, lane);
     }
     grp_sync<NT>();
     return tot;
-}
-
-__device__ __forceinline__ int wave_find_maskers(double2* buf, const PacTables* __restrict__ T,
-                                                 double drop, int lane, int* scratch, int16_t* rank) {
-    return grp_find_maskers<WAVE>(buf, T, drop, lane, scratch, rank);
-}
-
-// 2^(h + l) for a double-double exponent (|l| << ulp(h)): exp2(h) * (1 + l ln2)
-__device__ __forceinline__ double pac_exp2_dd(double h, double l) {
-    return pac_exp2(h) * __builtin_fma(l, PAC_LN2, 1.0);
-}
-
-// c + k * (a - b) as a double-double (TwoSum, TwoProduct via fma, TwoSum)
-__device__ __forceinline__ void dd_affine(double c, double k, double a, double b, double& hi, double& lo) {
-    double s = a - b;
-    double bb = s - a;
-    double err = (a - (s - bb)) + (-b - bb);
-    double ph = k * s;
-    double pl = __builtin_fma(k, s, -ph) + k * err;
-    double t = c + ph;
-    double cc = t - c;
-    double e2 = (c - (t - cc)) + (ph - cc);
-    hi = t;
-    lo = e2 + pl;
 }
 
 // wave-uniform results, returned in scalar registers (uniform loop bounds)
@@ -409,177 +551,115 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
-// Masking threshold (psychoac.py:447-456): for each MDCT line
-//   I(l) = sum_m 10^((spl_m(l) - 96)/10) + Intensity(Thresh(f_l)),  thr = SPL(I)
-// with spl_m(l) = SPL_m + spread(dz) - drop, dz = Bark(f_l) - Bark(f_m).
-// The sum splits by dz (the reference's slope selection, psychoac.py:111-116):
-//   dz >  1/2 (masker below the line): 2^(beta_m + ku_m (z_l - z_r)) per pair,
-//              beta_m = B_m + ku_m ((z_r - z_m) - 1/2) once per (row, masker);
-//              a leading run of maskers whose largest term over the row is
-//              below 2^-64 of a lower bound of every line's total is skipped;
-//   |dz| <= 1/2 (flat):                E_m = 2^B_m                no exp;
-//   dz < -1/2 (masker above the line): 2^(B_m + KL (z_m - 1/2 - z_r)) * 2^(KL (z_r - z_l))
-//              -- the lower slope is the constant -27 dB/Bark, so these terms
-//              factor into per-row suffix sums over maskers (one exp2 per
-//              masker per row instead of per line), exponents in double-double.
-// Every line adds its terms in ascending masker order; the loops are split so
-// that only the ragged ends of each zone need a per-lane test.  Values agree
-// with the direct sum to ~1e-15 relative.  Lane owns line l = 64 r + lane.
-// beta: 512 doubles of LDS private to the calling wave.
 // diagnostic build (-DPAC_ROWPROF): cycle and size counters of the masking rows
 #ifdef PAC_ROWPROF
 __device__ unsigned long long pac_rowprof[1024 * 16];   // spread over 1024 lines: no hot address
 #define RP_T(v) long long v = (long long)__builtin_amdgcn_s_memtime()
-#define RP_ADD(i, x) do { if (lane == 0) atomicAdd(&pac_rowprof[(blockIdx.x & 1023) * 16 + (i)], (unsigned long long)(x)); } while (0)
+#define RP_ADD(i_, v_) do { if (lane == 0) atomicAdd(&pac_rowprof[(blockIdx.x & 1023) * 16 + (i_)], (unsigned long long)(v_)); } while (0)
 #else
 #define RP_T(v) do {} while (0)
-#define RP_ADD(i, x) do {} while (0)
+#define RP_ADD(i_, v_) do {} while (0)
 #endif
 
-__device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, const PacTables* __restrict__ T,
-                                                   int lane, int r, double* beta, const int16_t* rank) {
-    const double* mz = mk_z(const_cast<double2*>(buf));
-    const double* mB = mk_B(const_cast<double2*>(buf));
-    const double* mku = mk_ku(const_cast<double2*>(buf));
-    const double* mE = mk_E(const_cast<double2*>(buf));
+// Masking threshold of MDCT row r (lines l = 64 r + lane) by one wave from the
+// masker lists: thr(l) = SPL(I(l) + Intensity(Thresh(f_l))).
+__device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm, const PacTables* __restrict__ T,
+                                                   int lane, int r) {
     const int l = r * WAVE + lane;
     const double zl = T->bark_line[l];
-    const double zr = T->bark_line[r * WAVE];          // row reference = smallest z
-    // U = #{m : zl - z_m > 1/2}, V = #{m : zl - z_m >= -1/2} (prefixes: z_m ascending),
-    // from the host-built bin bounds and the maskers' bin ranks
-    const int U = rank[T->mask_ku[l]];
-    const int V = rank[T->mask_kv[l]];
+    const double zr = T->bark_line[r * WAVE];           // smallest z of the row
+    const double zt = T->bark_line[r * WAVE + WAVE - 1];
+    const int U = L.rank[T->mask_ku[l]];
+    const int V = L.rank[T->mask_kv[l]];
     RP_T(t0);
-    // --- lower side: suffix sums of P_m = 2^(B_m + KL (z_m - 1/2 - zr)) over m >= vmin,
-    //     gathered at each lane's V by a cross-lane shuffle (no LDS)
-    const int vmin = wave_min_i(V);
-    double carry = 0.0, sv = 0.0;
-    for (int top = nm; top > vmin; top -= WAVE) {
-        const int m = top - WAVE + lane;
-        double x = 0.0;
-        if (m >= vmin) {
-            double h, lo2;
-            dd_affine(mB[m], PAC_KL, mz[m] - 0.5, zr, h, lo2);
-            x = pac_exp2_dd(h, lo2);
-        }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {            // inclusive suffix scan in the chunk
-            double y = __shfl_down(x, o, WAVE);
-            if (lane + o < 64) x += y;
-        }
-        const double tot = __shfl(x, 0, WAVE);
-        const int idx = V - (top - WAVE);
-        const double g = __shfl(x, idx & 63, WAVE) + carry;
-        if (idx >= 0 && idx < WAVE) sv = g;
-        carry += tot;
-    }
-    double lower = 0.0;
-    if (V < nm) {
-        double h, lo2;
-        dd_affine(0.0, -PAC_KL, zl, zr, h, lo2);
-        lower = sv * pac_exp2_dd(h, lo2);
-    }
+    // flat zone [U, V): difference of the dd prefix sums (positive terms)
+    double fs, fe;
+    two_sum(L.pfh[V], -L.pfh[U], fs, fe);
+    const double flat = fs + (fe + (L.pfl[V] - L.pfl[U]));
+    // lower side and the quiet maskers of the upper side: factored sums
+    const double lower = L.sl[V] * T->pow_mkl[l];
+    const double upq = L.su[U] * T->pow_kl[l];
+    const double tiq = T->tiq[l];
     RP_T(t1);
-    // --- flat zone [U, V), ascending: ragged head, common middle, ragged tail
-    double flat = 0.0;
-    const int umin = wave_min_i(U), umax = wave_max_i(U), vmax = wave_max_i(V);
-    const int fa = umax < vmax ? umax : vmax;
-    const int fb = fa > vmin ? fa : vmin;
-    const int span = wave_max_i(V - U);           // longest flat zone of the row
-    if (span < vmax - umin) {                     // each lane walks its own zone
-        for (int i = 0; i < span; ++i) {
-            const int m = U + i;
-            const double e = mE[m < V ? m : 0];
-            flat += (m < V) ? e : 0.0;
+    // loud maskers below the line: loud-list ranks [0, Ul)
+    const int Ul = L.lpre[U];
+    const int umin = wave_min_i(Ul), umax = wave_max_i(Ul);
+    double up = 0.0;
+    int m0 = umax, ua = umax;
+    bool direct = true;
+    int D = -1;
+    if (umax > 0) {
+        const double lb = wave_ext_f64<false>(((upq + flat) + lower) + tiq);   // I(l) >= lb on every lane
+        // floor(log2 lb) - 64 from the exponent field: a conservative cut
+        const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
+        for (int base = 0; base < umax; base += WAVE) {   // first loud masker that is not negligible
+            const int m = base + lane;
+            int keep = 1;
+            if (m < umax) {
+                const double ku = L.lku[m];
+                const double t = __builtin_fma(fmax((zr - L.lz[m]) - 0.5, 0.0), ku, L.lB[m]);
+                keep = !(ku < 0.0 && t < l2cut);
+            }
+            const unsigned long long kb = __ballot(keep);
+            if (kb) { m0 = base + __builtin_ctzll(kb); break; }
         }
-    } else {                                      // or the row's union of zones
-        for (int m = umin; m < fa; ++m) {
-            const double e = mE[m];
-            flat += (m >= U && m < V) ? e : 0.0;
-        }
-        for (int m = fa; m < fb; ++m) flat += mE[m];   // U <= umax <= m < vmin <= V on every lane
-        for (int m = fb; m < vmax; ++m) {
-            const double e = mE[m];
-            flat += (m >= U && m < V) ? e : 0.0;
-        }
+        m0 = __builtin_amdgcn_readfirstlane(m0 < umax ? m0 : umax);
     }
     RP_T(t2);
-    // --- upper side, ascending
-    const double tiq = T->tiq[l];
-    const double lb = wave_ext_f64<false>(tiq + flat + lower);   // I(l) >= lb on every lane
-    // floor(log2 lb) - 64 from the exponent field: a conservative cut
-    const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
-    int m0 = umax;                    // first masker that is not negligible (64 tested at once)
-    for (int base = 0; base < umax; base += WAVE) {
-        const int m = base + lane;
-        int keep = 1;
-        if (m < umax) {
-            const double ku = mku[m];
-            const double t = __builtin_fma(fmax((zr - mz[m]) - 0.5, 0.0), ku, mB[m]);
-            keep = !(ku < 0.0 && t < l2cut);
-        }
-        const unsigned long long kb = __ballot(keep);
-        if (kb) { m0 = base + __builtin_ctzll(kb); break; }
-    }
-    m0 = __builtin_amdgcn_readfirstlane(m0 < umax ? m0 : umax);
-    RP_T(t3);
-    // exponents relative to the row middle: 2^(beta_m + ku_m (z_l - z_mid))
-    const double zm = 0.5 * (zr + T->bark_line[r * WAVE + WAVE - 1]);
-    for (int m = m0 + lane; m < umax; m += WAVE)
-        beta[m] = __builtin_fma((zm - mz[m]) - 0.5, mku[m], mB[m]);
-    wave_sync();
+    // exponents relative to the row middle: 2^(beta_m + ku_m (z_l - z_mid)),
+    // beta_m = B_m + ku_m ((z_mid - z_m) - 1/2)
+    const double zm = 0.5 * (zr + zt);
     const double dl = zl - zm;
-    double up = 0.0;
-    const int ua = umin > m0 ? (umin < umax ? umin : umax) : m0;
-    // Maskers [m0, ua) lie below every line of the row.  Their sum factors as
+    ua = umin > m0 ? (umin < umax ? umin : umax) : m0;
+    // Loud maskers [m0, ua) lie below every line of the row.  Their sum factors as
     //   2^(kc dl) * sum_d (dl ln2)^d / d! * S_d,   S_d = sum_m 2^beta_m (ku_m - kc)^d,
     // kc the middle of their slopes: the Taylor series of 2^((ku_m - kc) dl),
     // truncated where its remainder is below 2^-57 of every term.
-    bool direct = true;
     if (ua - m0 >= PAC_MOM_MIN) {
         double kmn = INFINITY, kmx = -INFINITY;
         for (int m = m0 + lane; m < ua; m += WAVE) {
-            const double k = mku[m];
+            const double k = L.lku[m];
             kmn = fmin(kmn, k);
             kmx = fmax(kmx, k);
         }
         kmn = wave_ext_f64<false>(kmn);
         kmx = wave_ext_f64<true>(kmx);
-        // max |z_l - z_mid| over the row (ascending z: an end line)
-        const double adl = fmax(zm - zr, T->bark_line[r * WAVE + WAVE - 1] - zm);
+        const double adl = fmax(zm - zr, zt - zm);       // max |z_l - z_mid| over the row
         const double kc = 0.5 * (kmn + kmx);
         const double eps = (0.5 * (kmx - kmn) * adl) * PAC_LN2 * 1.0000001;
         // smallest D with e^eps eps^(D+1)/(D+1)! <= 2^-57 (uniform): lane j tests
         // eps against its bound; PAC_MOM_DMAX + 1 (no moment form) past the table
         const unsigned long long ok = __ballot(eps <= T->mom_eps[lane]);
-        const int D = ok ? (int)__builtin_ctzll(ok) : PAC_MOM_DMAX + 1;
-#ifdef PAC_ROWPROF
-        RP_ADD(8, D);
-#endif
+        D = ok ? (int)__builtin_ctzll(ok) : PAC_MOM_DMAX + 1;
         if (D <= PAC_MOM_DMAX) {
             direct = false;
             const double x = dl * PAC_LN2;
             const double invl = T->inv_int[lane];      // 1/j in lane j
-            double acc = 0.0, q = 1.0;
-            if (ua - m0 <= 2 * WAVE) {                 // two maskers per lane, in registers
-                const int ma = m0 + lane, mb = ma + WAVE;
-                double p0 = 0.0, c0 = 0.0, p1 = 0.0, c1 = 0.0;
-                if (ma < ua) { p0 = pac_exp2(beta[ma]); c0 = mku[ma] - kc; }
-                if (mb < ua) { p1 = pac_exp2(beta[mb]); c1 = mku[mb] - kc; }
-                for (int d = 0; d <= D; ++d) {
-                    acc = __builtin_fma(wave_sum_f64(p0 + p1), q, acc);
-                    p0 *= c0;
-                    p1 *= c1;
-                    q = (q * x) * readlane_f64(invl, d + 1);
+            double acc = 0.0;
+            // the sum is linear in the moments: groups of PAC_MOM_K maskers per lane
+            for (int g0 = m0; g0 < ua; g0 += PAC_MOM_K * WAVE) {
+                double pk[PAC_MOM_K], ck[PAC_MOM_K];
+#pragma unroll
+                for (int k = 0; k < PAC_MOM_K; ++k) {
+                    const int m = g0 + k * WAVE + lane;
+                    pk[k] = 0.0;
+                    ck[k] = 0.0;
+                    if (m < ua) {
+                        const double ku = L.lku[m];
+                        pk[k] = pac_exp2(__builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m]));
+                        ck[k] = ku - kc;
+                    }
                 }
-            } else {
-                for (int m = m0 + lane; m < ua; m += WAVE) beta[m] = pac_exp2(beta[m]);   // own slots
+                const int K = (ua - g0 + WAVE - 1) / WAVE;       // wave-uniform
+                double q = 1.0;
                 for (int d = 0; d <= D; ++d) {
                     double part = 0.0;
-                    for (int m = m0 + lane; m < ua; m += WAVE) {
-                        const double p = beta[m];
-                        part += p;
-                        beta[m] = p * (mku[m] - kc);
+#pragma unroll
+                    for (int k = 0; k < PAC_MOM_K; ++k) {
+                        if (k < K) {
+                            part += pk[k];
+                            pk[k] *= ck[k];
+                        }
                     }
                     acc = __builtin_fma(wave_sum_f64(part), q, acc);
                     q = (q * x) * readlane_f64(invl, d + 1);
@@ -588,31 +668,25 @@ __device__ __forceinline__ double wave_masking_row(const double2* buf, int nm, c
             up = acc * pac_exp2(kc * dl);
         }
     }
-    RP_T(t4);
+    RP_T(t3);
     if (direct) {
 #pragma unroll 2
-        for (int m = m0; m < ua; ++m)               // m < umin <= U on every lane
-            up += pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
+        for (int m = m0; m < ua; ++m) {             // m < umin <= Ul on every lane
+            const double ku = L.lku[m];
+            up += pac_exp2(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
+        }
     }
 #pragma unroll 2
     for (int m = ua; m < umax; ++m) {
-        const double t = pac_exp2(__builtin_fma(dl, mku[m], beta[m]));
-        up += (m < U) ? t : 0.0;
+        const double ku = L.lku[m];
+        const double t = pac_exp2(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
+        up += (m < Ul) ? t : 0.0;
     }
-    wave_sync();                                    // beta is rewritten by the next row
-    RP_T(t5);
+    RP_T(t4);
 #ifdef PAC_ROWPROF
     RP_ADD(0, 1); RP_ADD(1, t1 - t0); RP_ADD(2, t2 - t1); RP_ADD(3, t3 - t2); RP_ADD(4, t4 - t3);
-    RP_ADD(5, t5 - t4); RP_ADD(6, nm); RP_ADD(7, direct ? 0 : 1); RP_ADD(9, ua - m0);
-    RP_ADD(10, umax - ua); RP_ADD(11, vmax - umin); RP_ADD(12, nm - vmin); RP_ADD(13, m0);
-    RP_ADD(14, direct ? (ua - m0) : 0);
+    RP_ADD(5, nm); RP_ADD(6, L.misc[1]); RP_ADD(7, direct ? 0 : 1); RP_ADD(8, direct ? 0 : D);
+    RP_ADD(9, ua - m0); RP_ADD(10, umax - ua); RP_ADD(11, m0); RP_ADD(12, umax);
 #endif
-    return pac_spl(((up + flat) + lower) + tiq);
-}
-
-// all 16 rows by one wave
-__device__ __forceinline__ void wave_masking(const double2* buf, int nm, const PacTables* __restrict__ T,
-                                             int lane, double thr[16], double* beta, const int16_t* rank) {
-#pragma unroll 1
-    for (int r = 0; r < 16; ++r) thr[r] = wave_masking_row(buf, nm, T, lane, r, beta, rank);
+    return pac_spl((((up + upq) + flat) + lower) + tiq);
 }

@@ -550,11 +550,10 @@ static int report_rowprof(pac_ctx* c, hipStream_t s) {
     HIPCHK(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(pac_rowprof), all.size() * 8));
     for (int i = 0; i < 1024 * 16; i++) rp[i % 16] += all[i];
     const double n = (double)(rp[0] ? rp[0] : 1);
-    fprintf(stderr, "ROWPROF rows %llu  cyc lower %.0f flat %.0f skip %.0f mom %.0f direct+rag %.0f | nm %.1f "
-            "momrows %.3f D %.2f mom_n %.1f rag %.1f flatlen %.1f lowlen %.1f m0 %.1f direct_n %.1f\n",
+    fprintf(stderr, "ROWPROF rows %llu  cyc zones %.0f skip %.0f mom %.0f direct+rag %.0f | nm %.1f nloud %.1f "
+            "momrows %.3f D %.2f mom_n %.1f rag %.1f m0 %.1f umax %.1f\n",
             rp[0], rp[1] / n, rp[2] / n, rp[3] / n, rp[4] / n, rp[5] / n, rp[6] / n, rp[7] / n,
-            rp[8] / (double)(rp[7] ? rp[7] : 1), rp[9] / n, rp[10] / n, rp[11] / n, rp[12] / n, rp[13] / n,
-            rp[14] / n);
+            rp[8] / (double)(rp[7] ? rp[7] : 1), rp[9] / n, rp[10] / n, rp[11] / n, rp[12] / n);
     std::fill(all.begin(), all.end(), 0ull);
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pac_rowprof), all.data(), all.size() * 8));
 #else

@@ -374,59 +374,107 @@ __device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB, int1
     return L;
 }
 
-// exclusive prefix (dd) of h[0..n) in place into (h, l)[0..n], by one wave
-__device__ __forceinline__ void wave_scan_excl_dd(double* h, double* l, int n, int lane) {
-    double ch = 0.0, cl = 0.0;
-    for (int base = 0; base <= n; base += WAVE) {
-        const int m = base + lane;
-        double xh = m < n ? h[m] : 0.0, xl = 0.0;
+// DPP scans across the 64 lanes (gfx9 row_shr / row_bcast / wave_shr; lanes
+// without a source get the identity 0): inclusive prefix of a double, and of a
+// double-double (hi, lo) pair
+#define PAC_DPP_SHR(n) (0x110 + (n))
+#define PAC_DPP_WSHR1 0x138
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ void scan_step(double& x) { x += dpp_f64<CTRL, RM>(0.0, x); }
+__device__ __forceinline__ double wave_incl_scan_f64(double x) {
+    scan_step<PAC_DPP_SHR(1)>(x);
+    scan_step<PAC_DPP_SHR(2)>(x);
+    scan_step<PAC_DPP_SHR(4)>(x);
+    scan_step<PAC_DPP_SHR(8)>(x);
+    scan_step<PAC_DPP_BCAST15, 0xa>(x);
+    scan_step<PAC_DPP_BCAST31, 0xc>(x);
+    return x;
+}
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ void scan_step_dd(double& h, double& l) {
+    const double yh = dpp_f64<CTRL, RM>(0.0, h), yl = dpp_f64<CTRL, RM>(0.0, l);
+    dd_add(yh, yl, h, l, h, l);
+}
+__device__ __forceinline__ void wave_incl_scan_dd(double& h, double& l) {
+    scan_step_dd<PAC_DPP_SHR(1)>(h, l);
+    scan_step_dd<PAC_DPP_SHR(2)>(h, l);
+    scan_step_dd<PAC_DPP_SHR(4)>(h, l);
+    scan_step_dd<PAC_DPP_SHR(8)>(h, l);
+    scan_step_dd<PAC_DPP_BCAST15, 0xa>(h, l);
+    scan_step_dd<PAC_DPP_BCAST31, 0xc>(h, l);
+}
+
+// The three scans of the masker lists over m = 0..511 (elements zero at m >= nm),
+// one wave each (lane j owns 8 consecutive elements: an in-lane running sum,
+// a DPP scan of the lane totals, the lane's carry added back), no carries pass:
+//   pfh/pfl: exclusive prefix of E as an unnormalised double-double (hi, sum of
+//            the hi additions' rounding errors): |error| ~ n eps^2 of the prefix
+//   su:      exclusive prefix; sl: inclusive suffix (lanes own the segments in
+//            reverse order, so the lane scan runs downwards in m)
+__device__ __forceinline__ void wave_scan_flat_dd(const MaskerLists& L, int lane) {
+    const int m0 = 8 * lane;
+    double x[8], eh[8], el[8];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double yh = __shfl_up(xh, o, WAVE), yl = __shfl_up(xl, o, WAVE);
-            if (lane >= o) dd_add(yh, yl, xh, xl, xh, xl);
-        }
-        const double th = __shfl(xh, 63, WAVE), tl = __shfl(xl, 63, WAVE);
-        double eh = __shfl_up(xh, 1, WAVE), el = __shfl_up(xl, 1, WAVE);
-        if (lane == 0) { eh = 0.0; el = 0.0; }
-        double rh, rl;
-        dd_add(ch, cl, eh, el, rh, rl);
-        if (m <= n) { h[m] = rh; l[m] = rl; }
-        dd_add(ch, cl, th, tl, ch, cl);
+    for (int k = 0; k < 8; ++k) x[k] = L.pfh[m0 + k];
+    double rh = 0.0, rl = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        eh[k] = rh;
+        el[k] = rl;
+        double sx, e;
+        two_sum(rh, x[k], sx, e);
+        rh = sx;
+        rl += e;
+    }
+    double th = rh, tl = rl;      // inclusive scan of the lane totals
+    wave_incl_scan_dd(th, tl);
+    const double ch = dpp_f64<PAC_DPP_WSHR1>(0.0, th), cl = dpp_f64<PAC_DPP_WSHR1>(0.0, tl);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        double sx, e;
+        two_sum(ch, eh[k], sx, e);
+        L.pfh[m0 + k] = sx;
+        L.pfl[m0 + k] = (cl + el[k]) + e;
     }
 }
-// exclusive prefix of x[0..n) in place into x[0..n], by one wave
-__device__ __forceinline__ void wave_scan_excl(double* x, int n, int lane) {
-    double carry = 0.0;
-    for (int base = 0; base <= n; base += WAVE) {
-        const int m = base + lane;
-        double v = m < n ? x[m] : 0.0;
+__device__ __forceinline__ void wave_scan_excl8(double* v, int lane) {
+    const int m0 = 8 * lane;
+    double x[8];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_up(v, o, WAVE);
-            if (lane >= o) v += y;
-        }
-        const double t = __shfl(v, 63, WAVE);
-        double e = __shfl_up(v, 1, WAVE);
-        if (lane == 0) e = 0.0;
-        if (m <= n) x[m] = carry + e;
-        carry += t;
-    }
+    for (int k = 0; k < 8; ++k) x[k] = v[m0 + k];
+    double run = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { const double t = x[k]; x[k] = run; run += t; }
+    const double c = dpp_f64<PAC_DPP_WSHR1>(0.0, wave_incl_scan_f64(run));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[m0 + k] = c + x[k];
 }
-// suffix sums x[m] = sum_{k >= m} x_k in place, x[n] = 0, by one wave
-__device__ __forceinline__ void wave_scan_suffix(double* x, int n, int lane) {
-    double carry = 0.0;
-    for (int base = (n / WAVE) * WAVE; base >= 0; base -= WAVE) {
-        const int m = base + lane;
-        double v = m < n ? x[m] : 0.0;
+__device__ __forceinline__ void wave_scan_suffix8(double* v, int lane) {
+    const int m0 = 8 * (WAVE - 1 - lane);
+    double x[8];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_down(v, o, WAVE);
-            if (lane + o < 64) v += y;
-        }
-        const double t = __shfl(v, 0, WAVE);
-        if (m <= n) x[m] = carry + v;
-        carry += t;
+    for (int k = 0; k < 8; ++k) x[k] = v[m0 + k];
+    double run = 0.0;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) { run += x[k]; x[k] = run; }
+    const double c = dpp_f64<PAC_DPP_WSHR1>(0.0, wave_incl_scan_f64(run));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[m0 + k] = c + x[k];
+}
+template <int NT>
+__device__ __forceinline__ void grp_scan_lists(const MaskerLists& L, int tid) {
+    const int lane = tid & (WAVE - 1);
+    if constexpr (NT >= 3 * WAVE) {
+        const int w = tid / WAVE;
+        if (w == 0) wave_scan_flat_dd(L, lane);
+        else if (w == 1) wave_scan_suffix8(L.sl, lane);
+        else if (w == 2) wave_scan_excl8(L.su, lane);
+    } else {
+        wave_scan_flat_dd(L, lane);
+        wave_scan_suffix8(L.sl, lane);
+        wave_scan_excl8(L.su, lane);
     }
+    grp_sync<NT>();
 }
 
 // findpeaks (psychoac.py:158-191) on |X|^2 held in buf[k].x (the floor
@@ -513,12 +561,12 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
 #pragma unroll
     for (int i = 0; i < R * NW; ++i) { pre2[i] = nloud; nloud += cnt2[i]; }
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
+    for (int q = 0; q < R; ++q) {           // R * NT = 512: every slot, zero past nm
         const int idx = q * NT + tid;
+        L.pfh[idx] = rE[q];
+        L.sl[idx] = rPL[q];
+        L.su[idx] = rPU[q];
         if (idx < tot) {
-            L.pfh[idx] = rE[q];
-            L.sl[idx] = rPL[q];
-            L.su[idx] = rPU[q];
             const int j = pre2[q * NW + w] + __popcll(lb[q] & below);
             L.lpre[idx] = (int16_t)j;
             if ((lb[q] >> lane) & 1ull) { L.lz[j] = rz[q]; L.lB[j] = rB[q]; L.lku[j] = rku[q]; }
@@ -526,30 +574,25 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
     }
     if (tid == 0) { L.lpre[tot] = (int16_t)nloud; L.misc[1] = nloud; }
     grp_sync<NT>();
-    if constexpr (NW >= 3) {
-        if (w == 0) wave_scan_excl_dd(L.pfh, L.pfl, tot, lane);
-        else if (w == 1) wave_scan_suffix(L.sl, tot, lane);
-        else if (w == 2) wave_scan_excl(L.su, tot, lane);
-    } else {
-        wave_scan_excl_dd(L.pfh, L.pfl, tot, lane);
-        wave_scan_suffix(L.sl, tot, lane);
-        wave_scan_excl(L.su, tot, lane);
-    }
-    grp_sync<NT>();
+    grp_scan_lists<NT>(L, tid);
     return tot;
 }
 
-// wave-uniform results, returned in scalar registers (uniform loop bounds)
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w < v ? w : v; }
-    return __builtin_amdgcn_readfirstlane(v);
+// wave-uniform results, returned in scalar registers (uniform loop bounds);
+// DPP reductions as wave_sum_i (no LDS round trip)
+template <bool MAX>
+__device__ __forceinline__ int wave_ext_i(int v) {
+    auto f = [](int a, int b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_QXOR1, 0xf, 0xf, false));
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_QXOR2, 0xf, 0xf, false));
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_HMIRROR, 0xf, 0xf, false));
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_MIRROR, 0xf, 0xf, false));
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_BCAST15, 0xa, 0xf, false));
+    v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_BCAST31, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, WAVE); v = w > v ? w : v; }
-    return __builtin_amdgcn_readfirstlane(v);
-}
+__device__ __forceinline__ int wave_min_i(int v) { return wave_ext_i<false>(v); }
+__device__ __forceinline__ int wave_max_i(int v) { return wave_ext_i<true>(v); }
 
 // diagnostic build (-DPAC_ROWPROF): cycle and size counters of the masking rows
 #ifdef PAC_ROWPROF

@@ -38,6 +38,14 @@ __device__ __forceinline__ double dpp_f64(double old, double v) {
     const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, ROWMASK, 0xf, false);
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
+// full-row DPP patterns (every lane has a source): bound_ctrl, no old value
+template <int CTRL>
+__device__ __forceinline__ double dpp_full_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -51,10 +59,10 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 #define PAC_DPP_BCAST31 0x143
 // Wave-wide reductions (wave-uniform result; the same value on every lane)
 __device__ __forceinline__ double wave_sum_f64(double v) {
-    v += dpp_f64<PAC_DPP_QXOR1>(0.0, v);
-    v += dpp_f64<PAC_DPP_QXOR2>(0.0, v);
-    v += dpp_f64<PAC_DPP_HMIRROR>(0.0, v);
-    v += dpp_f64<PAC_DPP_MIRROR>(0.0, v);              // row sums
+    v += dpp_full_f64<PAC_DPP_QXOR1>(v);
+    v += dpp_full_f64<PAC_DPP_QXOR2>(v);
+    v += dpp_full_f64<PAC_DPP_HMIRROR>(v);
+    v += dpp_full_f64<PAC_DPP_MIRROR>(v);              // row sums
     v += dpp_f64<PAC_DPP_BCAST15, 0xa>(0.0, v);        // rows 1, 3 += rows 0, 2
     v += dpp_f64<PAC_DPP_BCAST31, 0xc>(0.0, v);        // rows 2, 3 += rows 0 + 1
     return readlane_f64(v, 63);
@@ -70,11 +78,12 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 }
 template <bool MAX>
 __device__ __forceinline__ double wave_ext_f64(double v) {
-    auto f = [](double a, double b) { return MAX ? fmax(a, b) : fmin(a, b); };
-    v = f(v, dpp_f64<PAC_DPP_QXOR1>(v, v));
-    v = f(v, dpp_f64<PAC_DPP_QXOR2>(v, v));
-    v = f(v, dpp_f64<PAC_DPP_HMIRROR>(v, v));
-    v = f(v, dpp_f64<PAC_DPP_MIRROR>(v, v));
+    // compare-select (no NaN canonicalisation: the operands are never NaN)
+    auto f = [](double a, double b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    v = f(v, dpp_full_f64<PAC_DPP_QXOR1>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_QXOR2>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_HMIRROR>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_MIRROR>(v));
     v = f(v, dpp_f64<PAC_DPP_BCAST15, 0xa>(v, v));
     v = f(v, dpp_f64<PAC_DPP_BCAST31, 0xc>(v, v));
     return readlane_f64(v, 63);
@@ -604,6 +613,40 @@ __device__ unsigned long long pac_rowprof[1024 * 16];   // spread over 1024 line
 #define RP_ADD(i_, v_) do {} while (0)
 #endif
 
+// One group of the moment form: KK loud maskers per lane (ranks g0 + 64 k +
+// lane < ua), sum_d q_d(l) S_d with q_d = x^d / d! (per line) and the moments
+// S_d = sum_m 2^beta_m (ku_m - kc)^d (wave sums).
+template <int KK>
+__device__ __forceinline__ double mom_group(const MaskerLists& L, const PacTables* __restrict__ T, int g0, int ua,
+                                            int lane, double zm, double kc, double x, int D) {
+    double pk[KK], ck[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+        const int m = g0 + k * WAVE + lane;
+        pk[k] = 0.0;
+        ck[k] = 0.0;
+        if (m < ua) {
+            const double ku = L.lku[m];
+            pk[k] = pac_exp2(__builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m]));
+            ck[k] = ku - kc;
+        }
+    }
+    double acc = 0.0, q = 1.0;
+    double inv = T->inv_int[1];          // 1/(d+1), loaded one iteration ahead
+    for (int d = 0; d <= D; ++d) {
+        const double inv_next = T->inv_int[d + 2];
+        double part = pk[0];
+#pragma unroll
+        for (int k = 1; k < KK; ++k) part += pk[k];
+#pragma unroll
+        for (int k = 0; k < KK; ++k) pk[k] *= ck[k];
+        acc = __builtin_fma(wave_sum_f64(part), q, acc);
+        q = (q * x) * inv;
+        inv = inv_next;
+    }
+    return acc;
+}
+
 // Masking threshold of MDCT row r (lines l = 64 r + lane) by one wave from the
 // masker lists: thr(l) = SPL(I(l) + Intensity(Thresh(f_l))).
 __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm, const PacTables* __restrict__ T,
@@ -677,36 +720,14 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
         if (D <= PAC_MOM_DMAX) {
             direct = false;
             const double x = dl * PAC_LN2;
-            const double invl = T->inv_int[lane];      // 1/j in lane j
             double acc = 0.0;
-            // the sum is linear in the moments: groups of PAC_MOM_K maskers per lane
+            // the sum is linear in the moments: groups of up to PAC_MOM_K maskers per lane
             for (int g0 = m0; g0 < ua; g0 += PAC_MOM_K * WAVE) {
-                double pk[PAC_MOM_K], ck[PAC_MOM_K];
-#pragma unroll
-                for (int k = 0; k < PAC_MOM_K; ++k) {
-                    const int m = g0 + k * WAVE + lane;
-                    pk[k] = 0.0;
-                    ck[k] = 0.0;
-                    if (m < ua) {
-                        const double ku = L.lku[m];
-                        pk[k] = pac_exp2(__builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m]));
-                        ck[k] = ku - kc;
-                    }
-                }
                 const int K = (ua - g0 + WAVE - 1) / WAVE;       // wave-uniform
-                double q = 1.0;
-                for (int d = 0; d <= D; ++d) {
-                    double part = 0.0;
-#pragma unroll
-                    for (int k = 0; k < PAC_MOM_K; ++k) {
-                        if (k < K) {
-                            part += pk[k];
-                            pk[k] *= ck[k];
-                        }
-                    }
-                    acc = __builtin_fma(wave_sum_f64(part), q, acc);
-                    q = (q * x) * readlane_f64(invl, d + 1);
-                }
+                if (K == 1) acc += mom_group<1>(L, T, g0, ua, lane, zm, kc, x, D);
+                else if (K == 2) acc += mom_group<2>(L, T, g0, ua, lane, zm, kc, x, D);
+                else if (K == 3) acc += mom_group<3>(L, T, g0, ua, lane, zm, kc, x, D);
+                else acc += mom_group<4>(L, T, g0, ua, lane, zm, kc, x, D);
             }
             up = acc * pac_exp2(kc * dl);
         }

@@ -234,7 +234,11 @@ class Job:
         self.ctx, self.p, self.fo, self.pcm_dev = ctx, p, fo, pcm_dev
         self.ns = len(fo) - 1
         self.blocks = int(sum(shard.blocks_of(fo[i + 1] - fo[i]) for i in range(self.ns)))
-        self.cap = int(ctx.L.pac_encode_bound(C.byref(p), self.ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
+        # the worst case (pac_encode_bound: 6 KB per master channel-block) would
+        # be 120 GB at 10^7 blocks; 1 KB per channel-block is > 3x the real
+        # average, and the library refuses (PAC_E_CAPACITY), never overflows
+        bound = int(ctx.L.pac_encode_bound(C.byref(p), self.ns, fo.ctypes.data_as(C.POINTER(C.c_int64))))
+        self.cap = min(bound, self.blocks * p.n_channels * 1024)
         self.out_dev = ctx.alloc(self.cap)
         self.so = None
 

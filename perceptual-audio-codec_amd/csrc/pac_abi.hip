@@ -476,17 +476,19 @@ static double bit_budget(const pac_params* p) {
     return b;
 }
 
-// worst-case bytes of one channel-block: '<L' + payload <= 4 + 25*8 + 16*1024
-// (+ 25 LRMS + sign bits + escape codes for master) bits
-static int64_t pac_encode_bound_per_channel_block() {
-    return 4 + (4 + 4 + 25 * 8 + 16 * 1024 + 25 + 1024 + 1024 * 16 + 7) / 8;
+// worst-case bytes of one channel-block: '<L' + payload.  Origin: 4 + 25*8 +
+// 16*1024 bits; master: PAC_MASTER_MAX_BITS (sign + code <= 47 bits per line)
+static int64_t pac_encode_bound_per_channel_block(int profile) {
+    const int64_t bits = profile == PAC_PROFILE_MASTER ? (int64_t)PAC_MASTER_MAX_BITS
+                                                       : (int64_t)(4 + PAC_NB * 8 + 16 * PAC_HALFN);
+    return 4 + (bits + 7) / 8;
 }
 
 extern "C" int64_t pac_encode_bound(const pac_params* p, int32_t n_streams, const int64_t* fo) {
     if (!p || !fo || n_streams < 0) return -1;
     int64_t blocks = 0;
     for (int s = 0; s < n_streams; s++) blocks += (fo[s + 1] - fo[s] + PAC_HALFN - 1) / PAC_HALFN + 1;
-    return blocks * p->n_channels * pac_encode_bound_per_channel_block();
+    return blocks * p->n_channels * pac_encode_bound_per_channel_block(p->profile);
 }
 
 __global__ void k_stream_offsets(const int64_t* __restrict__ off, const int64_t* __restrict__ blk_off,

@@ -415,22 +415,24 @@ __global__ __launch_bounds__(256) void k_scan_apply(const int32_t* __restrict__ 
 // bit packing helpers (MSB-first, bitpack.py:36-101), LDS u32 words
 // ---------------------------------------------------------------------------
 
+// The packed stream is kept as big-endian 32-bit words in LDS (stream bit i =
+// bit 31 - (i & 31) of word i >> 5), so a field of w <= 32 bits at bit p is at
+// most two atomicOr's; bytes come out as byte 3 - (i & 3) of word i >> 2.
 __device__ __forceinline__ void put_bits(uint32_t* words, int p, uint32_t v, int w) {
-    while (w > 0) {
-        int B = p >> 3, o = p & 7;
-        int take = (8 - o) < w ? (8 - o) : w;
-        uint32_t chunk = (v >> (w - take)) & ((1u << take) - 1u);
-        uint32_t byteval = chunk << (8 - o - take);
-        atomicOr(&words[B >> 2], byteval << (8 * (B & 3)));
-        p += take;
-        w -= take;
-    }
+    if (w <= 0) return;
+    const int o = p & 31;
+    const uint64_t x = (uint64_t)(v & (w >= 32 ? 0xffffffffu : ((1u << w) - 1u))) << (64 - o - w);
+    atomicOr(&words[p >> 5], (uint32_t)(x >> 32));
+    if (o + w > 32) atomicOr(&words[(p >> 5) + 1], (uint32_t)x);
+}
+__device__ __forceinline__ uint8_t be_byte(const uint32_t* words, int i) {
+    return (uint8_t)(words[i >> 2] >> (24 - 8 * (i & 3)));
 }
 
 __device__ __forceinline__ void store_block_bytes(uint8_t* __restrict__ out, const uint32_t* words,
                                                   int nbytes, int lane) {
     if (lane < 4) out[lane] = (uint8_t)((uint32_t)nbytes >> (8 * lane));   // '<L' nBytes
-    for (int i = lane; i < nbytes; i += WAVE) out[4 + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
+    for (int i = lane; i < nbytes; i += WAVE) out[4 + i] = be_byte(words, i);
 }
 
 #define PACK_WORDS 640   // >= (4 + 25*8 + 16*1024 + 25 + 1024)/32 bits
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
     if (off[g] + 4 + nbytes > cap) return;     // host reports PAC_E_CAPACITY from the total
     uint8_t* o = out + off[g];
     if (tid < 4) o[tid] = (uint8_t)((uint32_t)nbytes >> (8 * tid));   // '<L' nBytes
-    for (int i = tid; i < nbytes; i += FRONT_NT) o[4 + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
+    for (int i = tid; i < nbytes; i += FRONT_NT) o[4 + i] = be_byte(words, i);
 }
 
 // ---------------------------------------------------------------------------

@@ -434,137 +434,56 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
     if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
 }
 
-__device__ __forceinline__ int wave_excl_scan_i(int v, int lane, int* total) {
+// worst-case master channel-block: 8 + 25 * 8 + 25 bits + per line one sign bit
+// and a code of at most max(code length, escape length + ba) <= 30 + 16 bits
+// (pac_huffman_load rejects longer codes)
+#define PAC_MASTER_MAX_BITS (8 + PAC_NB * 8 + PAC_NB + PAC_HALFN * (1 + 30 + 16))
+#define PACK_WORDS_MASTER ((PAC_MASTER_MAX_BITS + 31) / 32)
+static_assert(PACK_WORDS_MASTER * 4 <= 16384, "packed words must fit a 16 KB line buffer");
+
+// exclusive prefix of an int across the wave by DPP; *total = the wave's sum
+__device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
     int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, WAVE);
-        if (lane >= o) x += y;
-    }
-    *total = __shfl(x, 63, WAVE);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(1), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(2), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(4), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(8), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST15, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST31, 0xc, 0xf, false);
+    *total = __builtin_amdgcn_readlane(x, 63);
     return x - v;
 }
 
-// PACFile.WriteDataBlock's packing of one master channel-block
-// (pacfile.py:288-351) by one wave: overall(4) tableID(4), per band
-// (ba?ba-1:0)(4) sf(4) [+ nLines sign bits + the Huffman codes], LRMS(25),
-// MSB-first into LDS words, then '<L nBytes' + payload to out (null: skip).
-__device__ void wave_pack_master(const PacTables* __restrict__ T, const PacHuffTables* __restrict__ H,
-                                 const PacMasterFields& F, int64_t g, int64_t gb, const double* ln,
-                                 uint32_t* words, int* bas, int* sfs, int* bstart, int* pre_at_lower, int lane,
-                                 uint8_t* __restrict__ out) {
-    for (int i = lane; i < PACK_WORDS; i += WAVE) words[i] = 0;
-    if (lane < PAC_NB) {
-        bas[lane] = F.ba[g * PAC_NB + lane];
-        sfs[lane] = F.sf[g * PAC_NB + lane];
-    }
-    wave_sync();
-    const int tb = F.tid[g] - 1;
-    // per line: sign + code of length clen (0 for ba == 0 bands)
-    uint32_t code[16], sgn[16];
-    int clen[16], esc[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int l = q * WAVE + lane;
-        const int b = T->band_of_line[l];
-        const int ba = bas[b];
-        clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
-        uint32_t m = 0;
-        if (ba) {
-            m = pac_mantissa(ln[l], sfs[b], ba);
-            const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
-            sgn[q] = (m >> (ba - 1)) & 1u;
-            const int L = H->len[tb][sym];
-            if (L) { clen[q] = L; code[q] = H->bits[tb][sym]; }
-            else { clen[q] = H->esc_len[tb] + ba; esc[q] = 1; code[q] = sym; }
-        }
-        if (F.dbg_code) {
-            const int64_t i = g * PAC_HALFN + l;
-            F.dbg_mant[i] = m;
-            F.dbg_code[i] = esc[q] ? (((uint64_t)H->esc_bits[tb] << ba) | code[q]) : (uint64_t)code[q];
-            F.dbg_len[i] = (uint8_t)clen[q];
-        }
-    }
-    // exclusive prefix of code lengths in line order (row q holds lines 64q..64q+63)
-    int pre[16];
-    int run = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        int tot;
-        const int ex = wave_excl_scan_i(clen[q], lane, &tot);
-        pre[q] = run + ex;
-        run += tot;
-    }
-    // band starts without code bits: 8 + sum_{b'<b} (8 + [ba>0] nl)
-    if (lane == 0) {
-        int p = 8;
-        for (int b = 0; b < PAC_NB; ++b) { bstart[b] = p; p += 8; if (bas[b]) p += T->nlines[b]; }
-        bstart[PAC_NB] = p;   // LRMS bits start (minus all code bits, added below)
-    }
-    // code bits of all earlier bands = the prefix at the band's first line
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int l = q * WAVE + lane;
-        const int b = T->band_of_line[l];
-        if (l == T->lower[b] && T->nlines[b]) pre_at_lower[b] = pre[q];
-    }
-    wave_sync();
-    if (lane == 0)      // empty bands: the prefix of the next band (or all code bits)
-        for (int b = PAC_NB - 1; b >= 0; --b)
-            if (!T->nlines[b]) pre_at_lower[b] = b == PAC_NB - 1 ? run : pre_at_lower[b + 1];
-    wave_sync();
-    if (lane == 0) {
-        put_bits(words, 0, (uint32_t)F.overall[g], 4);
-        put_bits(words, 4, (uint32_t)(tb + 1), 4);
-    }
-    if (lane < PAC_NB) {
-        const int b = lane, ba = bas[b];
-        const int p = bstart[b] + pre_at_lower[b];
-        put_bits(words, p, (uint32_t)(ba ? ba - 1 : 0), 4);
-        put_bits(words, p + 4, (uint32_t)sfs[b], 4);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int l = q * WAVE + lane;
-        const int b = T->band_of_line[l];
-        const int ba = bas[b];
-        if (!ba) continue;
-        const int p0 = bstart[b] + pre_at_lower[b] + 8;
-        put_bits(words, p0 + (l - T->lower[b]), sgn[q], 1);
-        const int pc = p0 + T->nlines[b] + (pre[q] - pre_at_lower[b]);
-        if (esc[q]) {
-            const int el = H->esc_len[tb];
-            put_bits(words, pc, H->esc_bits[tb], el);
-            put_bits(words, pc + el, code[q], ba);
-        } else {
-            put_bits(words, pc, code[q], clen[q]);
-        }
-    }
-    if (lane < PAC_NB) put_bits(words, bstart[PAC_NB] + run + lane, (uint32_t)F.lrms[gb * PAC_NB + lane], 1);
-    wave_sync();
-    if (out) store_block_bytes(out, words, F.nbytes[g] - 4, lane);
-}
-
-// Pass 2: one 256-thread workgroup per stereo block gb (XCD-aware order):
-// the block's MDCT lines are recomputed exactly as k_master_front computes
-// them (same kernels, same arithmetic: identical values), then waves 0 and 1
-// pack channels 0 and 1 at their final offsets.  A channel-block that would
-// end past cap is skipped; the host reports PAC_E_CAPACITY from the total.
+// Pass 2: one 256-thread workgroup per stereo block gb (XCD-aware order).
+// The block's MDCT lines are recomputed exactly as k_master_front computes
+// them (same functions, same arithmetic: identical values), then
+// PACFile.WriteDataBlock's packing of both channel-blocks (pacfile.py:288-351):
+// overall(4) tableID(4), per band (ba?ba-1:0)(4) sf(4) [+ nLines sign bits +
+// the Huffman codes], LRMS(25), MSB-first.  Waves 2c and 2c+1 pack channel c,
+// rows 0-7 and 8-15 of its lines; the code-bit prefix crosses the halves
+// through LDS.  A channel-block that would end past cap is skipped; the host
+// reports PAC_E_CAPACITY from the total.
 __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTables* __restrict__ T,
                                                      const PacHuffTables* __restrict__ H, PacMasterFields F,
                                                      int64_t nblocks, const int64_t* __restrict__ off,
                                                      uint8_t* __restrict__ out, int64_t cap) {
-    __shared__ double2 bufA[1024], bufB[1024];     // 32 KB: MDCT L / R, then the coded lines
-    __shared__ uint32_t words[2][PACK_WORDS];
+    __shared__ double2 bufA[1024], bufB[1024];     // 32 KB: MDCT L / R, the coded lines, then the packed words
     __shared__ int bas[2][PAC_NB], sfs[2][PAC_NB], bstart[2][PAC_NB + 1], pal[2][PAC_NB];
+    __shared__ int half_bits[2], tot_bits[2];
     __shared__ uint8_t lr[PAC_NB];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
+    const int c = w >> 1, h = w & 1;
     const int64_t gb = xcd_item(blockIdx.x, nblocks);
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
     if (tid < PAC_NB) lr[tid] = F.lrms[gb * PAC_NB + tid];
+    if (tid < 2 * PAC_NB) {
+        const int cc = tid / PAC_NB, b = tid % PAC_NB;
+        bas[cc][b] = F.ba[(gb * 2 + cc) * PAC_NB + b];
+        sfs[cc][b] = F.sf[(gb * 2 + cc) * PAC_NB + b];
+    }
     const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
     const double* XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
     const double gL = (double)(1 << F.overall[gb * 2]), gR = (double)(1 << F.overall[gb * 2 + 1]);
@@ -581,10 +500,110 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         L1[l] = ms ? S : xr;
     }
     __syncthreads();
-    if (w < 2) {
-        const int64_t g = gb * 2 + w;
-        const int nb = F.nbytes[g];
-        uint8_t* o = (off[g] + nb <= cap) ? out + off[g] : nullptr;
-        wave_pack_master(T, H, F, g, gb, w ? L1 : L0, words[w], bas[w], sfs[w], bstart[w], pal[w], lane, o);
+    const int64_t g = gb * 2 + c;
+    const int tb = F.tid[g] - 1;
+    const double* ln = c ? L1 : L0;
+    // this wave's 8 rows: sign + code of length clen per line (0 for ba == 0 bands)
+    uint32_t code[8], sgn[8];
+    int clen[8], esc[8], pre[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int l = (8 * h + q) * WAVE + lane;
+        const int b = T->band_of_line[l];
+        const int ba = bas[c][b];
+        clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
+        uint32_t m = 0;
+        if (ba) {
+            m = pac_mantissa(ln[l], sfs[c][b], ba);
+            const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
+            sgn[q] = (m >> (ba - 1)) & 1u;
+            const int L = H->len[tb][sym];
+            if (L) { clen[q] = L; code[q] = H->bits[tb][sym]; }
+            else { clen[q] = H->esc_len[tb] + ba; esc[q] = 1; code[q] = sym; }
+        }
+        if (F.dbg_code) {
+            const int64_t i = g * PAC_HALFN + l;
+            F.dbg_mant[i] = m;
+            F.dbg_code[i] = esc[q] ? (((uint64_t)H->esc_bits[tb] << ba) | code[q]) : (uint64_t)code[q];
+            F.dbg_len[i] = (uint8_t)clen[q];
+        }
     }
+    // exclusive prefix of the code lengths in line order
+    int run = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        int t;
+        pre[q] = run + wave_excl_scan_i(clen[q], &t);
+        run += t;
+    }
+    if (h == 0 && lane == 0) half_bits[c] = run;
+    __syncthreads();                  // every line read: bufA / bufB become the packed words
+    uint32_t* wd = reinterpret_cast<uint32_t*>(c ? bufB : bufA);
+    for (int i = tid; i < PACK_WORDS_MASTER; i += 256) {
+        reinterpret_cast<uint32_t*>(bufA)[i] = 0u;
+        reinterpret_cast<uint32_t*>(bufB)[i] = 0u;
+    }
+    if (h) {
+        const int hoff = half_bits[c];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pre[q] += hoff;
+        if (lane == 0) tot_bits[c] = hoff + run;
+    } else if (lane == 0) {           // band starts without code bits: 8 + sum_{b'<b} (8 + [ba>0] nl)
+        int p = 8;
+        for (int b = 0; b < PAC_NB; ++b) { bstart[c][b] = p; p += 8; if (bas[c][b]) p += T->nlines[b]; }
+        bstart[c][PAC_NB] = p;
+    }
+    // code bits of all earlier bands = the prefix at the band's first line
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int l = (8 * h + q) * WAVE + lane;
+        const int b = T->band_of_line[l];
+        if (l == T->lower[b] && T->nlines[b]) pal[c][b] = pre[q];
+    }
+    __syncthreads();
+    if (h == 0) {
+        if (lane == 0) {
+            put_bits(wd, 0, (uint32_t)F.overall[g], 4);
+            put_bits(wd, 4, (uint32_t)(tb + 1), 4);
+        }
+        if (lane < PAC_NB) {
+            const int b = lane, ba = bas[c][b];
+            int pa;
+            if (T->nlines[b]) {
+                pa = pal[c][b];
+            } else {                  // empty band: the prefix of the next non-empty one
+                int bb = b + 1;
+                while (bb < PAC_NB && !T->nlines[bb]) bb++;
+                pa = bb < PAC_NB ? pal[c][bb] : tot_bits[c];
+            }
+            const int p = bstart[c][b] + pa;
+            put_bits(wd, p, (uint32_t)(ba ? ba - 1 : 0), 4);
+            put_bits(wd, p + 4, (uint32_t)sfs[c][b], 4);
+        }
+    } else if (lane < PAC_NB) {
+        put_bits(wd, bstart[c][PAC_NB] + tot_bits[c] + lane, (uint32_t)lr[lane], 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int l = (8 * h + q) * WAVE + lane;
+        const int b = T->band_of_line[l];
+        const int ba = bas[c][b];
+        if (!ba) continue;
+        const int p0 = bstart[c][b] + pal[c][b] + 8;
+        put_bits(wd, p0 + (l - T->lower[b]), sgn[q], 1);
+        const int pc = p0 + T->nlines[b] + (pre[q] - pal[c][b]);
+        if (esc[q]) {
+            const int el = H->esc_len[tb];
+            put_bits(wd, pc, H->esc_bits[tb], el);
+            put_bits(wd, pc + el, code[q], ba);
+        } else {
+            put_bits(wd, pc, code[q], clen[q]);
+        }
+    }
+    __syncthreads();
+    const int nb = F.nbytes[g];
+    if (off[g] + nb > cap) return;
+    uint8_t* o = out + off[g];
+    if (h == 0 && lane < 4) o[lane] = (uint8_t)((uint32_t)(nb - 4) >> (8 * lane));   // '<L' nBytes
+    for (int i = h * WAVE + lane; i < nb - 4; i += 2 * WAVE) o[4 + i] = be_byte(wd, i);
 }

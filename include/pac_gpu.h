@@ -49,12 +49,25 @@ typedef struct {
     int32_t reserved;
 } pac_params;
 
-/* Cross-block encoder state of one stream: codingParams.extraBits
- * (codec.py:229,260) and huffman.bitDeposit (Huffman.py:262,353-371).
- * priorBlock (pacfile.py:265-268,282) is implicit in the stream's PCM. */
+/* Cross-block encoder state of one stream, so that a stream can be encoded
+ * across calls (streaming, or an origin stream split over GPUs with a one-hop
+ * halo): codingParams.extraBits (codec.py:229,260) and huffman.bitDeposit
+ * (Huffman.py:262,353-371), both MASTER only, and the framing flags:
+ *   PAC_STREAM_HAS_PRIOR  the stream's first 1024 frames are codingParams.
+ *                         priorBlock (pacfile.py:279-282): read as the first
+ *                         block's first half, not encoded as a hop of their own
+ *                         (without it the prior hop is zeros, pacfile.py:265-268)
+ *   PAC_STREAM_NO_FLUSH   no Close() flush block (pacfile.py:355-366): more
+ *                         hops follow in a later call
+ * A stream with n frames and flags f yields ceil((n - prior) / 1024) blocks
+ * plus the flush block unless NO_FLUSH. */
+#define PAC_STREAM_HAS_PRIOR 1
+#define PAC_STREAM_NO_FLUSH 2
 typedef struct {
     int64_t extra_bits;
     int64_t bit_deposit;
+    int32_t flags;
+    int32_t reserved;
 } pac_stream_state;
 
 /* Per-kernel device time of the last encode call (HIP events recorded on the
@@ -117,8 +130,8 @@ int pac_band_layout(int32_t sample_rate, int32_t n_lines_out[25]);
  * Writes each stream's data section ('<L nBytes' + payload per channel-block,
  * the bytes after the file header) back to back into out and its extent into
  * stream_byte_offsets (host, n_streams+1).  *_is_device: the pointer is
- * device memory (no PCIe copy).  states (host, n_streams, MASTER only,
- * nullable) are the reservoir in/out. */
+ * device memory (no PCIe copy).  states (host, n_streams, nullable): the
+ * framing flags in, the MASTER reservoir in/out (pac_stream_state). */
 int pac_encode_streams(pac_ctx *ctx, const pac_params *p, int32_t n_streams,
                        const int16_t *pcm, const int64_t *frame_offsets, int32_t pcm_is_device,
                        uint8_t *out, int64_t out_capacity, int32_t out_is_device,
@@ -150,6 +163,12 @@ int pac_decode_streams(pac_ctx *ctx, const pac_params *p, int32_t n_streams, con
                        const int64_t *stream_byte_offsets, int32_t data_is_device, int32_t preroll,
                        int16_t *pcm_out, int64_t pcm_capacity_frames, int32_t pcm_is_device,
                        double *float_out, int64_t *frame_offsets);
+
+/* The frame_offsets[n+1] pac_decode_streams produces for data sections in
+ * HOST memory, computed on the host (walks the '<L nBytes' prefixes; no device
+ * work).  PAC_E_ARG for a malformed section, like pac_decode_streams. */
+int pac_decode_layout(const pac_params *p, int32_t n_streams, const uint8_t *data,
+                      const int64_t *stream_byte_offsets, int32_t preroll, int64_t *frame_offsets);
 
 /* --- device buffers, sync, timing (benchmarks; data resident in HBM) ----- */
 int pac_device_alloc(pac_ctx *ctx, int64_t bytes, void **ptr);

@@ -31,8 +31,13 @@ class Params(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+STREAM_HAS_PRIOR = 1     # include/pac_gpu.h: first 1024 frames are the priorBlock
+STREAM_NO_FLUSH = 2      # no Close() flush block: the stream continues in a later call
+
+
 class StreamState(C.Structure):
-    _fields_ = [("extra_bits", C.c_int64), ("bit_deposit", C.c_int64)]
+    _fields_ = [("extra_bits", C.c_int64), ("bit_deposit", C.c_int64), ("flags", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class Timing(C.Structure):
@@ -80,6 +85,7 @@ def lib():
         "pac_encode_bound": (i64, [C.POINTER(Params), i32, C.POINTER(i64)]),
         "pac_decode_streams": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, i32, vp, i64,
                                          i32, vp, C.POINTER(i64)]),
+        "pac_decode_layout": (C.c_int, [C.POINTER(Params), i32, vp, C.POINTER(i64), i32, C.POINTER(i64)]),
         "pac_encode_block": (C.c_int, [vp, C.POINTER(Params), vp, C.POINTER(StreamState), vp, i64,
                                        C.POINTER(i64), C.POINTER(BlockFields)]),
         "pac_device_alloc": (C.c_int, [vp, i64, C.POINTER(vp)]),
@@ -197,10 +203,14 @@ class Context:
         args = [self.h, C.byref(params), ns, dptr, so.ctypes.data_as(C.POINTER(C.c_int64)),
                 int(bool(data_is_device)), int(bool(preroll))]
         fo_p = fo.ctypes.data_as(C.POINTER(C.c_int64))
-        if out is None:      # size query first (fills the frame offsets)
-            rc = self.L.pac_decode_streams(*args, None, 0, 0, None, fo_p)
-            if rc not in (PAC_OK, -6):
-                check(rc)
+        if out is None:      # output size: host-side layout walk (host data) or a size query (device data)
+            if data_is_device:
+                rc = self.L.pac_decode_streams(*args, None, 0, 0, None, fo_p)
+                if rc not in (PAC_OK, -6):
+                    check(rc)
+            else:
+                check(self.L.pac_decode_layout(C.byref(params), ns, dptr, so.ctypes.data_as(C.POINTER(C.c_int64)),
+                                               int(bool(preroll)), fo_p))
             frames = int(fo[-1])
             if out_is_device:
                 raise ValueError("out_is_device needs an out pointer")

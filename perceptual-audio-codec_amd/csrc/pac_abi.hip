@@ -244,6 +244,7 @@ struct pac_ctx {
     DevBuf<int32_t> nbytes;
     DevBuf<int64_t> off, tile_sums, grand_total, frame_off, blk_off, stream_off;
     DevBuf<int16_t> pcm_stage;
+    DevBuf<int32_t> lead;                   // per-stream prior-hop frames (PAC_STREAM_HAS_PRIOR)
     DevBuf<uint8_t> out_stage;
     DevBuf<double> fsrc;
     // master
@@ -261,6 +262,7 @@ struct pac_ctx {
     DevBuf<uint8_t> dec_data, dec_ba, dec_sf, dec_ov, dec_lrms;
     DevBuf<uint16_t> dec_codes;
     DevBuf<int64_t> dec_so, dec_cnt, dec_cbbase, dec_cboff, dec_nblk, dec_segbase, dec_fo;
+    DevBuf<int> dec_err;
     DevBuf<int16_t> dec_pcm;
     DevBuf<double> dec_fpcm;
     int64_t chunk_blocks = 65536;
@@ -314,11 +316,11 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
     c->dec_ov.release(); c->dec_lrms.release(); c->dec_codes.release(); c->dec_so.release();
     c->dec_cnt.release(); c->dec_cbbase.release(); c->dec_cboff.release(); c->dec_nblk.release();
-    c->dec_segbase.release(); c->dec_fo.release(); c->dec_pcm.release(); c->dec_fpcm.release();
+    c->dec_segbase.release(); c->dec_fo.release(); c->dec_err.release(); c->dec_pcm.release(); c->dec_fpcm.release();
     c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release(); c->prof.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
-    c->stream_off.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
+    c->stream_off.release(); c->lead.release(); c->pcm_stage.release(); c->out_stage.release(); c->fsrc.release();
     for (auto& e : c->ev) hipEventDestroy(e);
     for (auto& e : c->evpool) hipEventDestroy(e);
     for (auto& e : c->evs) hipEventDestroy(e);
@@ -771,10 +773,23 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     PacTables* T;
     if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
     const int nch = p->n_channels;
+    // blocks per stream: every hop after the (optional) carried priorBlock, plus
+    // the Close() flush block unless the stream continues in a later call
     std::vector<int64_t> blk(n_streams + 1);
+    std::vector<int32_t> lead(n_streams, 0);
+    bool any_lead = false;
     blk[0] = 0;
-    for (int s = 0; s < n_streams; s++)
-        blk[s + 1] = blk[s] + (frame_offsets[s + 1] - frame_offsets[s] + PAC_HALFN - 1) / PAC_HALFN + 1;
+    for (int s = 0; s < n_streams; s++) {
+        const int32_t fl = states ? states[s].flags : 0;
+        if (fl & ~(PAC_STREAM_HAS_PRIOR | PAC_STREAM_NO_FLUSH)) return set_err(PAC_E_ARG, "stream %d: flags", s);
+        int64_t n = frame_offsets[s + 1] - frame_offsets[s];
+        if (fl & PAC_STREAM_HAS_PRIOR) {   // a short prior is zero-padded, as the last hop (pcmfile.py:77-79)
+            lead[s] = PAC_HALFN;
+            any_lead = true;
+            n = n > PAC_HALFN ? n - PAC_HALFN : 0;
+        }
+        blk[s + 1] = blk[s] + (n + PAC_HALFN - 1) / PAC_HALFN + ((fl & PAC_STREAM_NO_FLUSH) ? 0 : 1);
+    }
     const int64_t nblocks = blk[n_streams];
     const int64_t G = nblocks * nch;
     if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
@@ -786,6 +801,15 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     HIPCHK(hipMemcpyAsync(c->frame_off.p, frame_offsets, (n_streams + 1) * sizeof(int64_t),
                           hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->blk_off.p, blk.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (any_lead) {
+        if ((rc = c->lead.ensure(n_streams))) return rc;
+        HIPCHK(hipMemcpyAsync(c->lead.p, lead.data(), n_streams * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    if (nblocks == 0) {       // nothing to encode (every stream continues, no new hop)
+        for (int k = 0; k <= n_streams; k++) stream_byte_offsets[k] = 0;
+        HIPCHK(hipStreamSynchronize(s));
+        return PAC_OK;
+    }
     const int16_t* pcm_dev = pcm;
     if (!pcm_is_device) {
         if ((rc = c->pcm_stage.ensure(nframes * nch + 1))) return rc;
@@ -800,7 +824,8 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         if ((rc = c->out_stage.ensure(want))) return rc;
         out_dev = c->out_stage.p;
     }
-    PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch, c->dbg};
+    PacSource src{pcm_dev, c->frame_off.p, c->blk_off.p, nullptr, n_streams, nch, c->dbg, nullptr,
+                  any_lead ? c->lead.p : nullptr};
     int64_t total = 0;
     if (master) {
         if ((rc = c->st_extra.ensure(n_streams)) || (rc = c->st_deposit.ensure(n_streams))) return rc;
@@ -870,7 +895,7 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
         (rc = c->blk_off.ensure(2)) || (rc = c->stream_off.ensure(2)))
         return rc;
     HIPCHK(hipMemcpyAsync(c->fsrc.p, full_block, G * PAC_N * sizeof(double), hipMemcpyHostToDevice, s));
-    PacSource src{nullptr, nullptr, c->blk_off.p, c->fsrc.p, 1, nch, 0};
+    PacSource src{nullptr, nullptr, c->blk_off.p, c->fsrc.p, 1, nch, 0, nullptr, nullptr};
     int64_t total = 0;
     std::vector<double> smr(PAC_NB * G);
     int32_t lrms[PAC_NB] = {0};
@@ -1070,6 +1095,33 @@ extern "C" int pac_last_timing(pac_ctx* c, pac_timing* out) {
 // decoder
 // ---------------------------------------------------------------------------
 
+// host-side layout of n data sections held in host memory: the output frame
+// offsets pac_decode_streams will produce (no device work, no staging)
+extern "C" int pac_decode_layout(const pac_params* p, int32_t n_streams, const uint8_t* data,
+                                 const int64_t* so, int32_t preroll, int64_t* frame_offsets) {
+    if (!p || !data || !so || !frame_offsets || n_streams < 1) return set_err(PAC_E_ARG, "null argument");
+    const int nch = p->n_channels;
+    if (nch < 1) return set_err(PAC_E_ARG, "n_channels %d", nch);
+    int64_t frames = 0;
+    for (int k = 0; k < n_streams; k++) {
+        int64_t pos = so[k], cnt = 0;
+        const int64_t end = so[k + 1];
+        while (pos + 4 <= end) {
+            const uint8_t* q = data + pos;
+            const uint32_t nb = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+            pos += 4 + (int64_t)nb;
+            cnt++;
+        }
+        if (pos != end || cnt % nch)
+            return set_err(PAC_E_ARG, "stream %d: malformed data section (channel-blocks %lld, %d channels)", k,
+                           (long long)cnt, nch);
+        frame_offsets[k] = frames;
+        frames += (cnt / nch + (preroll ? 1 : 0)) * PAC_HALFN;
+    }
+    frame_offsets[n_streams] = frames;
+    return PAC_OK;
+}
+
 extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_streams, const uint8_t* data,
                                   const int64_t* stream_byte_offsets, int32_t data_is_device, int32_t preroll,
                                   int16_t* pcm_out, int64_t pcm_capacity_frames, int32_t pcm_is_device,
@@ -1132,8 +1184,9 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     const int64_t G1 = G > 0 ? G : 1;
     if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(G1 * PAC_HALFN)) ||
         (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
-        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)))
+        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)))
         return rc;
+    HIPCHK(hipMemsetAsync(c->dec_err.p, 0, sizeof(int), s));
     HIPCHK(hipMemcpyAsync(c->dec_cbbase.p, cbb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->dec_nblk.p, nb.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->dec_segbase.p, segb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
@@ -1160,7 +1213,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     if (G) {
         hipLaunchKernelGGL(k_dec_index, dim3((n_streams + 255) / 256), dim3(256), 0, s, ddev, c->dec_so.p, n_streams,
                            c->dec_cbbase.p, c->dec_cboff.p);
-        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p};
+        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p, c->dec_err.p};
         hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, ddev, c->dec_cboff.p, G,
                            (int)master, T, master ? c->hdec_tab.p : nullptr, c->hdec, D);
         HIPCHK(hipGetLastError());
@@ -1179,7 +1232,11 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         HIPCHK(hipMemcpyAsync(pcm_out, pdev, frames * nch * sizeof(int16_t), hipMemcpyDeviceToHost, s));
     if (float_out && frames)
         HIPCHK(hipMemcpyAsync(float_out, fdev, frames * nch * sizeof(double), hipMemcpyDeviceToHost, s));
+    int derr = 0;
+    HIPCHK(hipMemcpyAsync(&derr, c->dec_err.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (derr)
+        return set_err(PAC_E_ARG, "malformed data section: a channel-block's fields run past its nBytes");
     if (c->timing) {
         hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);    // parse
         hipEventElapsedTime(&c->last.pack_ms, c->ev[1], c->ev[2]);     // synthesis

@@ -62,20 +62,28 @@ __global__ void k_dec_index(const uint8_t* __restrict__ data, const int64_t* __r
 }
 
 // MSB-first bit reader over one channel-block's bytes: aligned 32-bit loads
-// into a 64-bit buffer (one load per 32 bits consumed).  It runs ahead by up
-// to two words, i.e. it may load up to 8 bytes past the channel-block (bits
-// it never consumes): host data is staged with 8 bytes of padding, device
-// buffers come from hipMalloc (page granular).
+// into a 64-bit buffer (one load per 32 bits consumed).  Loads stop at the
+// word holding the channel-block's last byte (wend): past it the reader sees
+// zero bits, so a truncated or corrupt nBytes can never make it read outside
+// the data; the caller compares the bits consumed with 8 nBytes afterwards
+// (the reference's PackedBits raises on such input).
 struct DecBits {
     const uint32_t* w;     // aligned word stream
+    const uint32_t* wend;  // first word past the channel-block
     uint64_t buf;          // next bits, MSB first
     int nbuf;
     __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
-    __device__ __forceinline__ void init(const uint8_t* p, int64_t bit0) {
+    __device__ __forceinline__ uint32_t next_word() {
+        const uint32_t v = w < wend ? be(*w) : 0u;
+        ++w;
+        return v;
+    }
+    __device__ __forceinline__ void init(const uint8_t* p, int64_t bit0, const uint8_t* end) {
+        wend = reinterpret_cast<const uint32_t*>(((uintptr_t)end + 3) & ~(uintptr_t)3);
         const uintptr_t a = (uintptr_t)p + (uintptr_t)(bit0 >> 3);
         w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
         const int skip = (int)((a & 3) * 8 + (bit0 & 7));
-        buf = (uint64_t)be(*w++) << 32;
+        buf = (uint64_t)next_word() << 32;
         nbuf = 32;
         refill();
         buf <<= skip;
@@ -84,7 +92,7 @@ struct DecBits {
     }
     __device__ __forceinline__ void refill() {
         if (nbuf <= 32) {
-            buf |= (uint64_t)be(*w++) << (32 - nbuf);
+            buf |= (uint64_t)next_word() << (32 - nbuf);
             nbuf += 32;
         }
     }
@@ -135,6 +143,7 @@ struct PacDecWork {
     uint8_t* sf;
     uint8_t* overall;
     uint8_t* lrms;
+    int* err;           // set to 1 when a channel-block's fields run past its nBytes
 };
 
 __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ data,
@@ -145,8 +154,10 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint8_t* p = data + cb_off[g];
+    const uint32_t nbytes = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+    const uint8_t* end = p + 4 + nbytes;
     DecBits r;
-    r.init(p + 4, 0);
+    r.init(p + 4, 0, end);
     D.overall[g] = (uint8_t)r.read(4);
     const int id = master ? (int)r.read(4) - 1 : 0;
     uint16_t* codes = D.codes + g * PAC_HALFN;
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
             bit += (int64_t)nl * a;
         } else {
             DecBits sg;                            // nl sign bits, then nl Huffman codes
-            sg.init(p + 4, bit);
+            sg.init(p + 4, bit, end);
             r.advance(nl);
             bit += nl;
             const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
@@ -178,6 +189,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
     }
     if (master)
         for (int b = 0; b < PAC_NB; ++b) D.lrms[g * PAC_NB + b] = (uint8_t)r.read(1);
+    if (bits_consumed(r, p + 4) > 8 * (int64_t)nbytes) atomicOr(D.err, 1);
 }
 
 // vDequantize (quantize.py:345-376) + vDequantizeUniform (:118-145), 4 scale bits

@@ -12,6 +12,8 @@ struct PacSource {
     int n_ch;
     int dbg;                   // diagnostic phase switches (PAC_DEBUG_FLAGS), 0 in production
     long long* prof;           // diagnostic per-wave phase clocks (PAC_DEBUG_FLAGS & 16), else null
+    const int32_t* lead;       // [n_streams] frames before the first hop (1024: the stream carries its
+                               // priorBlock, PAC_STREAM_HAS_PRIOR), or null (all 0)
 };
 
 #define PAC_PROF_WG 4096       // workgroups sampled by the phase clocks

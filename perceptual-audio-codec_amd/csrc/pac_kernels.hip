@@ -52,7 +52,7 @@ __device__ __forceinline__ BlockRef locate(const PacSource& src, int64_t gb, int
     int64_t f0 = src.frame_off[s];
     r.pcm = src.pcm + f0 * src.n_ch;
     r.fsrc = nullptr;
-    r.first_frame = (b - 1) * PAC_HALFN;
+    r.first_frame = (b - 1) * PAC_HALFN + (src.lead ? src.lead[s] : 0);
     r.n_frames = src.frame_off[s + 1] - f0;
     return r;
 }

@@ -81,7 +81,15 @@ class PACFile(AudioFile):
         if getattr(self, "_dec", None) is None:
             data = self.fp.read()
             ctx = self.context or codec.default_context()
-            p = _lib.params(codingParams.sampleRate, codingParams.nChannels, self.profile)
+            # the header's values (the library rejects what the kernels do not
+            # support); Huffman-coded (.wak) iff a Huffman object is passed, as
+            # the master ReadDataBlock(codingParams, huffman) vs Origin's
+            # ReadDataBlock(codingParams)
+            prof = PROFILE_MASTER if huffman is not None else self.profile
+            p = _lib.params(codingParams.sampleRate, codingParams.nChannels, prof)
+            p.n_mdct_lines = int(codingParams.nMDCTLines)
+            p.n_scale_bits = int(codingParams.nScaleBits)
+            p.n_mant_size_bits = int(codingParams.nMantSizeBits)
             _, fo, fl = ctx.decode_streams(p, data, [0, len(data)], preroll=True, want_float=True)
             self._dec = fl
             self._pos = 0
@@ -139,6 +147,23 @@ def encode_streams(streams, sample_rate, profile=PROFILE_MASTER, context=None, s
     p = _lib.params(sample_rate, nch, profile)
     out, so = ctx.encode_streams(p, pcm, fo, states=states)
     return [out[so[i]:so[i + 1]].tobytes() for i in range(len(streams))]
+
+
+def encode_stream_parts(frames, sample_rate, parts, profile=PROFILE_MASTER, context=None):
+    """One stream encoded in `parts` calls (pac_amd.shard.split_stream): each
+    call carries its priorBlock and, for the master profile, the reservoir
+    state of the previous call (codingParams.extraBits, huffman.bitDeposit).
+    Returns the data section -- identical to one call's.  Origin parts could
+    run on different GPUs; here they run in order on one context."""
+    from .shard import split_stream
+    st = _lib.StreamState()
+    body = b""
+    for lo, hi, flags in split_stream(frames.shape[0], parts):
+        st.flags = flags
+        states = [st]
+        body += encode_streams([frames[lo:hi]], sample_rate, profile, context, states=states)[0]
+        st = states[0]
+    return body
 
 
 def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):

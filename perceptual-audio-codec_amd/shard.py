@@ -63,6 +63,31 @@ def encode_files(in_paths, out_paths, profile=1, context=None, rank=None, world=
     return mine
 
 
+def split_stream(n_frames, parts, n_mdct_lines=1024):
+    """Split ONE stream's hops into up to `parts` contiguous ranges (SURVEY.md
+    8(e), origin row: block ranges with a one-hop halo).  Returns a list of
+    (frame_lo, frame_hi, flags): part i encodes hops [h_i, h_i+1) from frames
+    [(h_i - 1) * 1024, h_i+1 * 1024) -- the first hop of that slice is the part's
+    priorBlock (STREAM_HAS_PRIOR), every part but the last omits the Close()
+    flush block (STREAM_NO_FLUSH).  The parts' data sections, concatenated in
+    order, are the one-call data section.  Origin parts are independent (any
+    rank, any order); master parts must run in order, each starting from the
+    previous part's reservoir state."""
+    from ._lib import STREAM_HAS_PRIOR, STREAM_NO_FLUSH
+    n = int(n_frames)
+    hops = (n + n_mdct_lines - 1) // n_mdct_lines
+    parts = max(1, min(int(parts), hops))
+    bounds = [hops * k // parts for k in range(parts + 1)]
+    out = []
+    for i in range(parts):
+        h0, h1 = bounds[i], bounds[i + 1]
+        lo = (h0 - 1) * n_mdct_lines if i > 0 else 0
+        hi = min(n, h1 * n_mdct_lines)
+        flags = (STREAM_HAS_PRIOR if i > 0 else 0) | (STREAM_NO_FLUSH if i < parts - 1 else 0)
+        out.append((lo, hi, flags))
+    return out
+
+
 def balance(block_counts, shards):
     loads = np.array([sum(int(block_counts[i]) for i in s) for s in shards], dtype=np.int64)
     return loads, (loads.max() / max(loads.mean(), 1e-9)) if len(loads) else 1.0

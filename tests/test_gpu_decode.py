@@ -110,3 +110,28 @@ def test_mono_and_three_channel_origin(ctx):
         got = pacfile.decode_streams([sec], 32000, nch, pacfile.PROFILE_ORIGIN, context=ctx)[0]
         ref = P.Oracle(32000, huffman=False).decode_data(P.ORIGIN, sec, nch)
         assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,prof", [("piano_test2.wak", pacfile.PROFILE_MASTER),
+                                       ("harpsichord.pac", pacfile.PROFILE_ORIGIN)])
+def test_corrupt_nbytes_is_refused(ctx, name, prof):
+    """A channel-block whose '<L nBytes' is cut short (its fields run past it)
+    makes the decoder raise PAC_E_ARG -- the reference's PackedBits raises --
+    and never read outside the data."""
+    from pac_amd import _lib
+    with open(fixture(name), "rb") as f:
+        b = bytearray(f.read())
+    fs, nch, ns, _, off = pacfile.parse_header(bytes(b))
+    # the largest channel-block: shrink its nBytes by 40 and drop the last 40
+    # bytes of its payload (the channel-blocks after it stay intact)
+    pos, big, bign = off, off, -1
+    while pos + 4 <= len(b):
+        n = int.from_bytes(b[pos:pos + 4], "little")
+        if n > bign:
+            big, bign = pos, n
+        pos += 4 + n
+    b[big:big + 4] = (bign - 40).to_bytes(4, "little")
+    del b[big + 4 + bign - 40:big + 4 + bign]
+    with pytest.raises(_lib.PacError) as e:
+        ctx.decode_streams(_lib.params(fs, nch, prof), bytes(b[off:]), [0, len(b) - off])
+    assert e.value.code == -1

@@ -218,3 +218,49 @@ def test_shard_plan_gloo_world2(tmp_path):
                         str(script)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "GLOO_OK" in r.stdout
+
+
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 5 * 1024, 37 * 1024 + 11])
+@pytest.mark.parametrize("parts", [1, 2, 3, 7])
+def test_split_stream_plan(n, parts):
+    """shard.split_stream: the parts cover every hop exactly once, each later
+    part carries the one-hop halo (its priorBlock) and only the last part
+    ends with the flush block."""
+    from pac_amd import shard, _lib
+    sp = shard.split_stream(n, parts)
+    hops = (n + 1023) // 1024
+    assert 1 <= len(sp) <= max(1, min(parts, hops))
+    covered = []
+    for i, (lo, hi, fl) in enumerate(sp):
+        prior = 1024 if fl & _lib.STREAM_HAS_PRIOR else 0
+        assert bool(fl & _lib.STREAM_HAS_PRIOR) == (i > 0)
+        assert bool(fl & _lib.STREAM_NO_FLUSH) == (i < len(sp) - 1)
+        first = (lo + prior) // 1024
+        nh = (max(hi - lo - prior, 0) + 1023) // 1024
+        covered += list(range(first, first + nh))
+        assert hi <= n and lo >= 0
+    assert covered == list(range(hops))
+
+
+@pytest.mark.parametrize("name,prof", [("piano_test2.wak", 1), ("harpsichord.pac", 0)])
+def test_decode_layout_on_host(name, prof):
+    """pac_decode_layout (host only, no GPU): the decoded frame count of a
+    reference file equals the oracle's decode, and a truncated section is
+    refused like the reference's reader refuses it."""
+    from pac_amd import _lib
+    import pyoracle as P
+    with open(fixture(name), "rb") as f:
+        b = f.read()
+    fs, nch, ns, nl, off = P.parse_pac_header(b)
+    data = np.frombuffer(b[off:], dtype=np.uint8)
+    so = np.array([0, len(data)], dtype=np.int64)
+    fo = np.zeros(2, dtype=np.int64)
+    p = _lib.params(fs, nch, prof)
+    L = _lib.lib()
+    P64 = C.POINTER(C.c_int64)
+    assert L.pac_decode_layout(C.byref(p), 1, data.ctypes.data, so.ctypes.data_as(P64), 0, fo.ctypes.data_as(P64)) == 0
+    o = P.Oracle(fs, huffman=bool(prof))
+    assert int(fo[1]) == o.decode_data(prof, b[off:], nch).shape[0]
+    so2 = np.array([0, len(data) - 3], dtype=np.int64)
+    assert L.pac_decode_layout(C.byref(p), 1, data.ctypes.data, so2.ctypes.data_as(P64), 0,
+                               fo.ctypes.data_as(P64)) == -1

@@ -614,6 +614,7 @@ static int run_origin(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
 static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     if (!c->timing) return;
     c->last.thr_ms = 0.f;
+    c->last.lrms_ms = 0.f;
     hipEventSynchronize(c->ev[4]);
     hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
     hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
@@ -702,7 +703,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             const int64_t B = (int64_t)gr.n_s * gr.S;
             if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
             if ((rc = mark(0, -1))) return rc;
-            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s0, src, T, K, ck);
+            hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
+            if ((rc = mark(0, 5))) return rc;
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
             if ((rc = mark(0, 0))) return rc;
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             HIPCHK(hipGetLastError());
@@ -735,7 +738,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s0));
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
-        float ph[5] = {0, 0, 0, 0, 0};
+        float ph[6] = {0, 0, 0, 0, 0, 0};
         for (int k = 0; k < 2; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
@@ -748,7 +751,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         c->last.alloc_ms = ph[2];
         c->last.pack_ms = ph[3];
         c->last.scan_ms = ph[4];
-        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4];   // the tail overlaps the next chunk
+        c->last.lrms_ms = ph[5];
+        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5];   // the tail overlaps the next chunk
         c->last.n_channel_blocks = G;
         c->last.out_bytes = 0;
     }

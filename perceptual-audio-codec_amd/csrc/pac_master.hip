@@ -84,7 +84,8 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 }
 
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                         PacMasterChunkBuf K, PacMasterChunk ck) {
+                                                         PacMasterChunkBuf K, PacMasterFields F,
+                                                         PacMasterChunk ck) {
     __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
     __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // FFT scratch, then loud list (region B)
     __shared__ int16_t rank[PAC_HALFN];
@@ -95,6 +96,27 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int v = (int)(item % 6);
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;     // uniform per workgroup
+    // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
+    // the M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
+    // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
+    __shared__ int rowmask;
+    if (tid == 0) rowmask = 0;
+    __syncthreads();
+    {
+        const int want = v >= 2 ? 1 : 0;
+        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+        int bits = 0;
+#pragma unroll
+        for (int i = 0; i < PAC_HALFN / FRONT_NT; ++i) {
+            const int l = i * FRONT_NT + tid;
+            if (l < lend && F.lrms[gb * PAC_NB + T->band_of_line[l]] == want) bits |= 1 << (l / WAVE);
+        }
+        bits = __builtin_amdgcn_readfirstlane(wave_or_i(bits));
+        if (lane == 0 && bits) atomicOr(&rowmask, bits);
+    }
+    __syncthreads();
+    const int rows = rowmask;
+    if (!rows) return;                                      // uniform per workgroup
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
@@ -113,6 +135,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
+        if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
         out[r * WAVE + lane] = wave_masking_row(L, nm, T, lane, r);
     }
 }
@@ -191,25 +214,20 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
     grp_sync<NT>();
 }
 
-// One 256-thread workgroup per stereo block: LRMS decision, MDCT L/R and
-// overall scales, M/S lines, MLD threshold combination, SMR selection and the
-// band maxima (LDS atomic max on order-preserving keys).
-__global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
-                                                      PacMasterChunkBuf K, PacMasterFields F,
-                                                      PacMasterChunk ck) {
+// One 256-thread workgroup per stereo block: the LRMS decision (codec.py:94-102)
+// |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band, over the complex FFT bins
+// of the raw (unwindowed) blocks, with numpy's pairwise sums.  It runs first so
+// that k_master_thr computes only the thresholds a band's coding mode uses.
+__global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTables* __restrict__ T,
+                                                     PacMasterFields F, PacMasterChunk ck) {
     __shared__ double2 bufA[1024], bufB[1024], bufC[1024];    // 48 KB
     __shared__ double2 leafv[2][64];
-    __shared__ uint8_t lrms_s[PAC_NB];
-    __shared__ unsigned long long key[6][32];    // SMR 0/1, |line| 0/1, max|X| L/R
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
-    if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
-
-    // --- LRMS: |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band (codec.py:94-102)
     grp_spectrum_cplx<256>([&](int i) { return rL(i); }, T, bufA, bufC, tid);
     grp_spectrum_cplx<256>([&](int i) { return rR(i); }, T, bufB, bufC, tid);
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
@@ -236,10 +254,28 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         const int n = 2 * T->nlines[tid];
         const double2 sd = np_csum_combine<5>(leafv[0], i0, n);
         const double2 ss = np_csum_combine<5>(leafv[1], i1, n);
-        const int v = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
-        lrms_s[tid] = (uint8_t)v;
-        F.lrms[gb * PAC_NB + tid] = (uint8_t)v;
+        F.lrms[gb * PAC_NB + tid] = (uint8_t)(hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0);
     }
+}
+
+// One 256-thread workgroup per stereo block: MDCT L/R and overall scales, M/S
+// lines, MLD threshold combination, SMR selection and the band maxima (LDS
+// atomic max on order-preserving keys).  Only the thresholds of each band's
+// coding mode are read (k_master_thr computes no others).
+__global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
+                                                      PacMasterChunkBuf K, PacMasterFields F,
+                                                      PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
+    __shared__ uint8_t lrms_s[PAC_NB];
+    __shared__ unsigned long long key[6][32];    // SMR 0/1, |line| 0/1, max|X| L/R
+    const int tid = threadIdx.x;
+    const int64_t j = blockIdx.x;
+    int64_t gb;
+    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    const BlockPcm rL(locate(src, gb, 0));
+    const BlockPcm rR(locate(src, gb, 1));
+    if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
+    if (tid < PAC_NB) lrms_s[tid] = F.lrms[gb * PAC_NB + tid];
     __syncthreads();
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
@@ -272,24 +308,23 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         const int l = i * 256 + tid;
         const double xl = __dmul_rn(xl4[i], gL), xr = __dmul_rn(xr4[i], gR);
         const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
-        const double bL = thr[0 * PAC_HALFN + l], bR = thr[1 * PAC_HALFN + l];
-        const double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
-        const double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
-        const double mld = T->mld[l];
-        const double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
-        const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
-        const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
-        const double c = bM < mldM ? bM : mldM;
-        const double thrS = bS > c ? bS : c;
         const int b = T->band_of_line[l];
         const int ms = l < lend ? lrms_s[b] : 0;
         double d0, d1;
         if (ms) {
+            const double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
+            const double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
+            const double mld = T->mld[l];
+            const double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
+            const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
+            const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
+            const double c = bM < mldM ? bM : mldM;
+            const double thrS = bS > c ? bS : c;
             d0 = (pac_spl(4. * (M * M)) - offL) - thrM;
             d1 = (pac_spl(4. * (S * S)) - offR) - thrS;
         } else {
-            d0 = (pac_spl(4. * (xl * xl)) - offL) - bL;
-            d1 = (pac_spl(4. * (xr * xr)) - offR) - bR;
+            d0 = (pac_spl(4. * (xl * xl)) - offL) - thr[0 * PAC_HALFN + l];
+            d1 = (pac_spl(4. * (xr * xr)) - offR) - thr[1 * PAC_HALFN + l];
         }
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;

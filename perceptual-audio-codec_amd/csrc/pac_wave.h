@@ -600,6 +600,15 @@ __device__ __forceinline__ int wave_ext_i(int v) {
     v = f(v, __builtin_amdgcn_update_dpp(v, v, PAC_DPP_BCAST31, 0xc, 0xf, false));
     return __builtin_amdgcn_readlane(v, 63);
 }
+__device__ __forceinline__ int wave_or_i(int v) {
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_QXOR1, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_QXOR2, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_HMIRROR, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_MIRROR, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_BCAST15, 0xa, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, PAC_DPP_BCAST31, 0xc, 0xf, false);
+    return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ int wave_min_i(int v) { return wave_ext_i<false>(v); }
 __device__ __forceinline__ int wave_max_i(int v) { return wave_ext_i<true>(v); }
 

@@ -392,6 +392,17 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
             h->bits[tid - 1][sym] = b;
         }
     }
+    for (int sym = 0; sym < PAC_NSYM; sym++) {
+        uint64_t v = 0;
+        for (int t = 0; t < PAC_NTAB; t++) {
+            if (h->len[t][sym] > 30) {
+                free(h);
+                return set_err(PAC_E_TABLES, "code longer than 30 bits");
+            }
+            v |= (uint64_t)h->len[t][sym] << (5 * t);
+        }
+        h->lens10[sym] = v;
+    }
     HIPCHK(hipSetDevice(c->device));
     if (!c->huff && hipMalloc((void**)&c->huff, sizeof(PacHuffTables)) != hipSuccess) {
         free(h);
@@ -713,7 +724,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             HIPCHK(hipEventRecord(c->evs[k], s0));
             HIPCHK(hipStreamWaitEvent(s1, c->evs[k], 0));
             if ((rc = mark(1, -1))) return rc;
-            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)gr.n_s), dim3(64), 0, s1, T, c->huff, K, F,
+            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((gr.n_s + 3) / 4)), dim3(WAVE), 0, s1, T,
+                               c->huff, K, F,
                                c->blk_off.p, ck, c->st_extra.p, c->st_deposit.p, budget);
             HIPCHK(hipGetLastError());
             if ((rc = mark(1, 2))) return rc;

@@ -346,67 +346,124 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     }
 }
 
-// --- master BitAlloc (bitalloc.py:129-184), band b on lane b ---------------
-// Each round gives one bit to the first band with the largest smr - 6 bits
-// among the still-valid bands (wave max + ballot: the serial loop's
-// first-index tie break); the stop test uses the max of smr - 6 (bits - 1)
-// over all bands, as the reference does.  Returns the bits left minus extra;
-// *ba_lane = this lane's band allocation.
-__device__ long bitalloc_master(const double* __restrict__ smr_g, const uint8_t* lrms,
-                                const PacTables* __restrict__ T, double bitBudget, long extra,
-                                int maxMantBits, int lane, int* ba_lane) {
-    const bool band = lane < PAC_NB;
-    const double smr = band ? smr_g[lane] : 0.0;
-    const int nl = band ? T->nlines[lane] : 0;
-    const int lr = band ? lrms[lane] : 0;
-    int bits = 0;
-    bool valid = band;
+// --- the reservoir tail: 16 lanes (one DPP row) per stream -----------------
+// Reductions inside a row of 16 lanes: every lane of the row gets the result.
+template <int CTRL>
+__device__ __forceinline__ int dpp_row_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true); }
+__device__ __forceinline__ int row_sum_i(int v) {
+    v += dpp_row_i<PAC_DPP_QXOR1>(v);
+    v += dpp_row_i<PAC_DPP_QXOR2>(v);
+    v += dpp_row_i<PAC_DPP_HMIRROR>(v);
+    v += dpp_row_i<PAC_DPP_MIRROR>(v);
+    return v;
+}
+// (value, band, bits) with the larger value winning, the lower band on a tie
+// (np.argmax's first index over ascending bands)
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(double& v, int& b, int& n) {
+    const double ov = dpp_full_f64<CTRL>(v);
+    const int ob = dpp_row_i<CTRL>(b), on = dpp_row_i<CTRL>(n);
+    const bool take = ov > v || (ov == v && ob < b);
+    v = take ? ov : v;
+    b = take ? ob : b;
+    n = take ? on : n;
+}
+__device__ __forceinline__ void row_argmax(double& v, int& b, int& n) {
+    argmax_step<PAC_DPP_QXOR1>(v, b, n);
+    argmax_step<PAC_DPP_QXOR2>(v, b, n);
+    argmax_step<PAC_DPP_HMIRROR>(v, b, n);
+    argmax_step<PAC_DPP_MIRROR>(v, b, n);
+}
+
+// master BitAlloc (bitalloc.py:129-184) by the 16 lanes of a row: lane q owns
+// bands q and q + 16.  Each round gives one bit to the first band with the
+// largest smr - 6 bits among the still-valid bands; the stop test uses the
+// max of smr - 6 (bits - 1) over ALL bands as the reference does -- that is
+// max(best valid, best frozen) + 6, the frozen (invalidated) bands' values no
+// longer changing.  The winner's bits, LRMS flag and line count travel with
+// the reduction (no memory access inside the loop).  *ba0 / *ba1 = the lane's
+// bands' allocation; returns the bits left minus extra (same in every lane of
+// the row).
+__device__ __forceinline__ long bitalloc_master_row(const double* __restrict__ smr_g,
+                                                    const uint8_t* __restrict__ lrms,
+                                                    const PacTables* __restrict__ T, double bitBudget, long extra,
+                                                    int maxMantBits, int q, int* ba0, int* ba1) {
+    const int b0 = q, b1 = q + 16;
+    const bool has1 = b1 < PAC_NB;
+    const double s0 = smr_g[b0], s1 = has1 ? smr_g[b1] : 0.0;
+    const int nl0 = T->nlines[b0], nl1 = has1 ? T->nlines[b1] : 0;
+    const int info0 = (lrms[b0] << 5) | (nl0 << 6), info1 = has1 ? ((lrms[b1] << 5) | (nl1 << 6)) : 0;
+    int n0 = 0, n1 = 0;
+    bool v0 = true, v1 = has1;
     long total = (long)(bitBudget + (double)extra);
-    while (__ballot(valid)) {
-        const double v = smr - bits * 6.;
-        const double best = wave_ext_f64<true>(valid ? v : -INFINITY);
-        const unsigned long long win = __ballot(valid && v == best);
-        const int im = __builtin_ctzll(win);
-        const double g = wave_ext_f64<true>(band ? smr - (bits - 1) * 6. : -INFINITY);
-        const int nli = __builtin_amdgcn_readlane(nl, im);
-        const int lri = __builtin_amdgcn_readlane(lr, im);
-        const int bi = __builtin_amdgcn_readlane(bits, im);
-        bool drop = g < (lri ? -5.0 : -15.0);
+    double frozen = -INFINITY;
+    while (true) {
+        double v = v0 ? s0 - n0 * 6. : -INFINITY;
+        int b = v0 ? b0 : 64, p = info0 | n0;
+        if (v1 && s1 - n1 * 6. > v) { v = s1 - n1 * 6.; b = b1; p = info1 | n1; }
+        row_argmax(v, b, p);
+        if (b >= PAC_NB) break;                       // no valid band left (uniform in the row)
+        const int n = p & 31, lri = (p >> 5) & 1, nli = p >> 6;
+        const double gall = fmax(v, frozen) + 6.0;
+        bool drop = gall < (lri ? -5.0 : -15.0);
+        double after = v;
         if (total - nli >= 0) {
-            if (lane == im) bits += 1;
+            if (b == b0) n0 += 1;
+            if (b == b1) n1 += 1;
             total -= nli;
-            drop |= bi + 1 >= maxMantBits;
+            drop |= n + 1 >= maxMantBits;
+            after = v - 6.0;
         } else {
             drop = true;
         }
-        if (lane == im && drop) valid = false;
+        if (drop) {
+            if (b == b0) v0 = false;
+            if (b == b1) v1 = false;
+            frozen = fmax(frozen, after);
+        }
     }
     int back = 0;
-    if (bits == 1) { back = nl; bits = 0; }
-    total += wave_sum_i(back);
-    *ba_lane = bits;
+    if (n0 == 1) { back += nl0; n0 = 0; }
+    if (has1 && n1 == 1) { back += nl1; n1 = 0; }
+    total += row_sum_i(back);
+    *ba0 = n0;
+    *ba1 = n1;
     return total - extra;
 }
 
-// One wave per stream of the chunk: the serial reservoir chain over the
-// stream's blocks t0 .. t0+S-1 and each channel-block's byte count.
+// 16 lanes (one DPP row) per stream of the chunk, four streams per wave: the
+// serial reservoir chain over the stream's blocks t0 .. t0+S-1 --
+// withdrawBits, the two BitAlloc calls with the extraBits carry
+// (codec.py:222-260), scale factors, StripSignBits + Huffman.encodeData's
+// length scoring of the 10 tables (Huffman.py:274-309), depositBits
+// (codec.py:111-124) -- and each channel-block's byte count.
 __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict__ T,
                                                     const PacHuffTables* __restrict__ H,
                                                     PacMasterChunkBuf K, PacMasterFields F,
                                                     const int64_t* __restrict__ blk_off, PacMasterChunk ck,
                                                     int64_t* __restrict__ st_extra,
                                                     int64_t* __restrict__ st_deposit, double bitBudget) {
-    __shared__ int ba_s[PAC_NB], sf_s[PAC_NB];
+    __shared__ uint8_t ba_s[4][32], sf_s[4][32];
+    // a latency-bound chain sharing the SIMDs with the next chunk's threshold
+    // waves: issue ahead of them
+    __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x;
-    const int sl = blockIdx.x;
+    const int r = lane >> 4, q = lane & 15;
+    const int sl = blockIdx.x * 4 + r;
+    if (sl >= ck.n_s) return;                          // whole rows only
     const int s = ck.s_first + sl;
-    const int64_t b0 = blk_off[s];
-    const int64_t len = blk_off[s + 1] - b0;
+    const int64_t bb0 = blk_off[s];
+    const int64_t len = blk_off[s + 1] - bb0;
     const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
     long extra = st_extra[s], deposit = st_deposit[s];
+    const int b0 = q, b1 = q + 16;
+    const bool has1 = b1 < PAC_NB;
+    int esc[PAC_NTAB];
+#pragma unroll
+    for (int tb = 0; tb < PAC_NTAB; ++tb) esc[tb] = H->esc_len[tb];
     for (int64_t t = ck.t0; t < t_end; ++t) {
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
-        const int64_t gb = b0 + t;
+        const int64_t gb = bb0 + t;
         // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
         long e = 0;
         if (deposit > 10) { e = deposit / 100; deposit -= e; }
@@ -415,58 +472,73 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
         long dep_add = 0;
         for (int ch = 0; ch < 2; ++ch) {
             const int64_t gl = j * 2 + ch, g = gb * 2 + ch;
-            int ba;
-            const long diff = bitalloc_master(K.smr + gl * PAC_NB, F.lrms + gb * PAC_NB, T, bitBudget, extra, 16,
-                                              lane, &ba);
-            extra += diff;
-            if (lane < PAC_NB) {
-                ba_s[lane] = ba;
-                const int sf = pac_scale_factor(K.bandpeak[gl * PAC_NB + lane], ba);
-                sf_s[lane] = sf;
-                F.ba[g * PAC_NB + lane] = (uint8_t)ba;
-                F.sf[g * PAC_NB + lane] = (uint8_t)sf;
+            int a0, a1;
+            extra += bitalloc_master_row(K.smr + gl * PAC_NB, F.lrms + gb * PAC_NB, T, bitBudget, extra, 16, q,
+                                         &a0, &a1);
+            const int f0 = pac_scale_factor(K.bandpeak[gl * PAC_NB + b0], a0);
+            const int f1 = has1 ? pac_scale_factor(K.bandpeak[gl * PAC_NB + b1], a1) : 0;
+            ba_s[r][b0] = (uint8_t)a0;
+            sf_s[r][b0] = (uint8_t)f0;
+            F.ba[g * PAC_NB + b0] = (uint8_t)a0;
+            F.sf[g * PAC_NB + b0] = (uint8_t)f0;
+            if (has1) {
+                ba_s[r][b1] = (uint8_t)a1;
+                sf_s[r][b1] = (uint8_t)f1;
+                F.ba[g * PAC_NB + b1] = (uint8_t)a1;
+                F.sf[g * PAC_NB + b1] = (uint8_t)f1;
             }
+            int nsign = (a0 ? T->nlines[b0] : 0) + (has1 && a1 ? T->nlines[b1] : 0);
+            int orig = a0 * T->nlines[b0] + (has1 ? a1 * T->nlines[b1] : 0);
             wave_sync();
-            // StripSignBits + Huffman.encodeData scoring of the 10 tables
+            // Huffman scoring: lines l = 16 i + q of the 1024, eight at a time (one
+            // gather of the ten tables' lengths per line, the loads in flight together)
             const double* ln = K.lines + gl * PAC_HALFN;
             int acc[PAC_NTAB];
 #pragma unroll
             for (int tb = 0; tb < PAC_NTAB; ++tb) acc[tb] = 0;
-            int nsign = 0, orig = 0;
-            for (int q = 0; q < 16; ++q) {
-                const int l = q * WAVE + lane;
-                const int b = T->band_of_line[l];
-                const int bal = ba_s[b];
-                if (!bal) continue;
-                const uint32_t m = pac_mantissa(ln[l], sf_s[b], bal);
-                const uint32_t sym = m & ((1u << (bal - 1)) - 1u);
-                nsign += 1;
-                orig += bal;
+            for (int l0 = q; l0 < PAC_HALFN; l0 += 16 * 8) {
+                uint64_t lens[8];
+                int bal[8];
 #pragma unroll
-                for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                    const int L = H->len[tb][sym];
-                    acc[tb] += L ? L : H->esc_len[tb] + bal;
+                for (int u = 0; u < 8; ++u) {
+                    const int l = l0 + 16 * u;
+                    const int b = T->band_of_line[l];
+                    const int ba = ba_s[r][b];
+                    bal[u] = ba;
+                    lens[u] = 0;
+                    if (ba) {
+                        const uint32_t sym = pac_mantissa(ln[l], sf_s[r][b], ba) & ((1u << (ba - 1)) - 1u);
+                        lens[u] = H->lens10[sym];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (!bal[u]) continue;
+#pragma unroll
+                    for (int tb = 0; tb < PAC_NTAB; ++tb) {
+                        const int L = (int)((lens[u] >> (5 * tb)) & 31u);
+                        acc[tb] += L ? L : esc[tb] + bal[u];
+                    }
                 }
             }
-            nsign = wave_sum_i(nsign);
-            orig = wave_sum_i(orig);
+            nsign = row_sum_i(nsign);
+            orig = row_sum_i(orig);
             int best = 0, bestid = 1;
 #pragma unroll
             for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                const int v = wave_sum_i(acc[tb]);
+                const int v = row_sum_i(acc[tb]);
                 if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
             }
             dep_add += (long)orig - ((long)best + nsign + 4);
-            const int nbits = 8 + 8 * PAC_NB + nsign + best + PAC_NB;
-            if (lane == 0) {
+            if (q == 0) {
                 F.tid[g] = (uint8_t)bestid;
-                F.nbytes[g] = 4 + (nbits + 7) / 8;
+                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + 7) / 8;
             }
-            wave_sync();
+            wave_sync();                               // ba_s / sf_s rewritten by the next channel
         }
         deposit += dep_add;     // depositBits per channel (codec.py:120)
     }
-    if (lane == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
+    if (q == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
 }
 
 // worst-case master channel-block: 8 + 25 * 8 + 25 bits + per line one sign bit

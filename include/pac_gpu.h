@@ -170,6 +170,42 @@ int pac_decode_streams(pac_ctx *ctx, const pac_params *p, int32_t n_streams, con
 int pac_decode_layout(const pac_params *p, int32_t n_streams, const uint8_t *data,
                       const int64_t *stream_byte_offsets, int32_t preroll, int64_t *frame_offsets);
 
+/* --- WAV ingest / egress on the device ------------------------------------
+ * PCMFile.ReadFileHeader (pcmfile.py:32-65): the 4-byte-step scan for 'fmt '
+ * and 'data' as the reference does it.  status 0, or the reference's raise:
+ * -1 not RIFF, -2 no 'fmt ', -3 not PCM, -4 not 16-bit, -5 no 'data'.
+ * frames = the frames the encode driver reads: num_samples, plus one hop when
+ * num_samples is an exact multiple of 1024 and bytes follow the data
+ * (PACFile.WriteFileHeader bumps the shared numSamples, pacfile.py:240-242;
+ * the hop holds extra_bytes of the file, zero-padded, pcmfile.py:77-79). */
+typedef struct {
+    int32_t sample_rate, n_channels, bits_per_sample, status;
+    int64_t num_samples;    /* header frames (numSamples)                  */
+    int64_t data_offset;    /* byte offset of the first sample in the file */
+    int64_t frames;         /* frames the encoder reads                    */
+    int64_t extra_bytes;
+} pac_wav_info;
+
+/* Scan n WAV files held back to back in blob (file_offsets[n+1], host). */
+int pac_wav_scan(pac_ctx *ctx, int32_t n_files, const uint8_t *blob, const int64_t *file_offsets,
+                 int32_t blob_is_device, pac_wav_info *info);
+
+/* The encode driver (pacfile.py:430-499) for n WAV files held back to back in
+ * blob: header scan, frame gather (+ the quirk hop) into the encoder's PCM
+ * and pac_encode_streams, all on the device.  Every file must match p's
+ * sample rate and channel count.  info_out (host, nullable) gets the scan. */
+int pac_encode_wav(pac_ctx *ctx, const pac_params *p, int32_t n_files, const uint8_t *blob,
+                   const int64_t *file_offsets, int32_t blob_is_device, uint8_t *out, int64_t out_capacity,
+                   int32_t out_is_device, int64_t *stream_byte_offsets, pac_stream_state *states,
+                   pac_wav_info *info_out);
+
+/* The decode driver's output WAV files (pacfile.py:478-499): pac_decode_streams
+ * + PCMFile.WriteFileHeader from each coded file's numSamples (num_samples,
+ * host, n) + the frames, back to back into out (wav_offsets[n+1], host). */
+int pac_decode_wav(pac_ctx *ctx, const pac_params *p, int32_t n_streams, const uint8_t *data,
+                   const int64_t *stream_byte_offsets, int32_t data_is_device, const int64_t *num_samples,
+                   uint8_t *out, int64_t out_capacity, int32_t out_is_device, int64_t *wav_offsets);
+
 /* --- device buffers, sync, timing (benchmarks; data resident in HBM) ----- */
 int pac_device_alloc(pac_ctx *ctx, int64_t bytes, void **ptr);
 int pac_device_free(pac_ctx *ctx, void *ptr);

@@ -40,6 +40,12 @@ class StreamState(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+class WavInfo(C.Structure):       # pac_wav_info
+    _fields_ = [("sample_rate", C.c_int32), ("n_channels", C.c_int32), ("bits_per_sample", C.c_int32),
+                ("status", C.c_int32), ("num_samples", C.c_int64), ("data_offset", C.c_int64),
+                ("frames", C.c_int64), ("extra_bytes", C.c_int64)]
+
+
 class Timing(C.Structure):
     _fields_ = [("front_ms", C.c_float), ("alloc_ms", C.c_float), ("scan_ms", C.c_float),
                 ("pack_ms", C.c_float), ("total_ms", C.c_float),
@@ -86,6 +92,11 @@ def lib():
         "pac_decode_streams": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, i32, vp, i64,
                                          i32, vp, C.POINTER(i64)]),
         "pac_decode_layout": (C.c_int, [C.POINTER(Params), i32, vp, C.POINTER(i64), i32, C.POINTER(i64)]),
+        "pac_wav_scan": (C.c_int, [vp, i32, vp, C.POINTER(i64), i32, C.POINTER(WavInfo)]),
+        "pac_encode_wav": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, vp, i64, i32,
+                                     C.POINTER(i64), C.POINTER(StreamState), C.POINTER(WavInfo)]),
+        "pac_decode_wav": (C.c_int, [vp, C.POINTER(Params), i32, vp, C.POINTER(i64), i32, C.POINTER(i64), vp, i64,
+                                     i32, C.POINTER(i64)]),
         "pac_encode_block": (C.c_int, [vp, C.POINTER(Params), vp, C.POINTER(StreamState), vp, i64,
                                        C.POINTER(i64), C.POINTER(BlockFields)]),
         "pac_device_alloc": (C.c_int, [vp, i64, C.POINTER(vp)]),
@@ -226,6 +237,67 @@ class Context:
         if out_is_device:
             return out, fo, (fl[:frames] if want_float else None)
         return out[:frames], fo, (fl[:frames] if want_float else None)
+
+    # --- WAV ingest / egress on the device --------------------------------
+    def wav_scan(self, blob, file_offsets, blob_is_device=False):
+        fo = np.ascontiguousarray(file_offsets, dtype=np.int64)
+        n = len(fo) - 1
+        info = (WavInfo * n)()
+        ptr = blob if blob_is_device else np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8)).ctypes.data
+        keep = blob
+        check(self.L.pac_wav_scan(self.h, n, ptr, fo.ctypes.data_as(C.POINTER(C.c_int64)), int(bool(blob_is_device)),
+                                  info))
+        del keep
+        return list(info)
+
+    def encode_wav(self, params, blob, file_offsets, blob_is_device=False, out=None, out_capacity=None,
+                   out_is_device=False, states=None):
+        """pac_encode_wav: WAV files back to back in blob (bytes, or a device
+        pointer).  Returns (out, stream byte offsets, [WavInfo])."""
+        fo = np.ascontiguousarray(file_offsets, dtype=np.int64)
+        n = len(fo) - 1
+        info = (WavInfo * n)()
+        if blob_is_device:
+            ptr = blob
+        else:
+            arr = np.frombuffer(blob, dtype=np.uint8)
+            ptr = arr.ctypes.data
+        if out is None:
+            # >= pac_encode_bound of any 16-bit file: per 2048 bytes at most one
+            # mono block (or half a stereo one) of <= 6054 bytes, + flush/quirk hops
+            cap = sum((int(fo[i + 1] - fo[i]) // 2048 + 3) * 6100 for i in range(n))
+            out = np.empty(cap, dtype=np.uint8)
+        if isinstance(out, np.ndarray):
+            out_ptr, cap = out.ctypes.data, (out.nbytes if out_capacity is None else out_capacity)
+        else:
+            out_ptr, cap = out, out_capacity
+        so = np.zeros(n + 1, dtype=np.int64)
+        st = (StreamState * n)(*states) if states is not None else None
+        check(self.L.pac_encode_wav(self.h, C.byref(params), n, ptr, fo.ctypes.data_as(C.POINTER(C.c_int64)),
+                                    int(bool(blob_is_device)), out_ptr, int(cap), int(bool(out_is_device)),
+                                    so.ctypes.data_as(C.POINTER(C.c_int64)), st, info))
+        if states is not None:
+            for i in range(n):
+                states[i] = st[i]
+        return out, so, list(info)
+
+    def decode_wav(self, params, data, stream_offsets, num_samples):
+        """pac_decode_wav: data sections (bytes) -> the decode driver's WAV files
+        (bytes, back to back) and their offsets."""
+        so = np.ascontiguousarray(stream_offsets, dtype=np.int64)
+        n = len(so) - 1
+        ns = np.ascontiguousarray(num_samples, dtype=np.int64)
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        fo = np.zeros(n + 1, dtype=np.int64)
+        P64 = C.POINTER(C.c_int64)
+        check(self.L.pac_decode_layout(C.byref(params), n, buf.ctypes.data, so.ctypes.data_as(P64), 0,
+                                       fo.ctypes.data_as(P64)))
+        cap = int(fo[-1]) * params.n_channels * 2 + 44 * n
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        wo = np.zeros(n + 1, dtype=np.int64)
+        check(self.L.pac_decode_wav(self.h, C.byref(params), n, buf.ctypes.data, so.ctypes.data_as(P64), 0,
+                                    ns.ctypes.data_as(P64), out.ctypes.data, cap, 0, wo.ctypes.data_as(P64)))
+        return out, wo
 
     def encode_block(self, params, full_block, state=None):
         fb = np.ascontiguousarray(full_block, dtype=np.float64)

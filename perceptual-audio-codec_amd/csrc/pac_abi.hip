@@ -20,6 +20,7 @@
 #include "pac_kernels.hip"
 #include "pac_master.hip"
 #include "pac_decode.hip"
+#include "pac_wav.hip"
 
 #define PAC_VERSION 100
 
@@ -263,6 +264,10 @@ struct pac_ctx {
     DevBuf<uint16_t> dec_codes;
     DevBuf<int64_t> dec_so, dec_cnt, dec_cbbase, dec_cboff, dec_nblk, dec_segbase, dec_fo;
     DevBuf<int> dec_err;
+    // WAV ingest / egress
+    DevBuf<uint8_t> wav_blob, wav_pcm, wav_out;
+    DevBuf<int64_t> wav_foff, wav_fo, wav_segb, wav_ns, wav_wo;
+    DevBuf<PacWavInfo> wav_info;
     DevBuf<int16_t> dec_pcm;
     DevBuf<double> dec_fpcm;
     int64_t chunk_blocks = 65536;
@@ -316,7 +321,9 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
     c->dec_ov.release(); c->dec_lrms.release(); c->dec_codes.release(); c->dec_so.release();
     c->dec_cnt.release(); c->dec_cbbase.release(); c->dec_cboff.release(); c->dec_nblk.release();
-    c->dec_segbase.release(); c->dec_fo.release(); c->dec_err.release(); c->dec_pcm.release(); c->dec_fpcm.release();
+    c->dec_segbase.release(); c->dec_fo.release(); c->dec_err.release();
+    c->wav_blob.release(); c->wav_pcm.release(); c->wav_out.release(); c->wav_foff.release();
+    c->wav_fo.release(); c->wav_segb.release(); c->wav_ns.release(); c->wav_wo.release(); c->wav_info.release(); c->dec_pcm.release(); c->dec_fpcm.release();
     c->smr.release(); c->bandpeak.release(); c->overall.release(); c->ba.release(); c->prof.release();
     c->sf.release(); c->nbytes.release(); c->off.release(); c->tile_sums.release();
     c->grand_total.release(); c->frame_off.release(); c->blk_off.release();
@@ -1262,5 +1269,142 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         c->last.n_channel_blocks = G;
         c->last.out_bytes = frames * nch * 2;
     }
+    return PAC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// WAV ingest / egress on the device
+// ---------------------------------------------------------------------------
+
+static_assert(sizeof(PacWavInfo) == sizeof(pac_wav_info), "pac_wav_info layout");
+
+static const char* wav_status_msg(int st) {     // the reference's raises (pcmfile.py:36-51)
+    switch (st) {
+        case PAC_WAV_NOT_RIFF: return "File opened for PCMFile is not a RIFF file!";
+        case PAC_WAV_NO_FMT: return "Didn't find WAV file 'fmt ' chunk following RIFF file header";
+        case PAC_WAV_NOT_PCM: return "Opened a non-PCM WAV file as a PCMFile";
+        case PAC_WAV_NOT_16BIT: return "PCMFile was not 16-bits per sample";
+        case PAC_WAV_NO_DATA: return "Didn't find WAV file 'data' chunk following 'fmt ' chunk";
+        default: return "malformed WAV file";
+    }
+}
+
+// stage (if host) and scan n files; the blob's device pointer in *dev
+static int wav_scan_dev(pac_ctx* c, int32_t n, const uint8_t* blob, const int64_t* foff, int32_t blob_is_device,
+                        const uint8_t** dev, pac_wav_info* info) {
+    int rc;
+    if (!c || !blob || !foff || !info || n < 1) return set_err(PAC_E_ARG, "null argument or n_files < 1");
+    if (foff[0] != 0) return set_err(PAC_E_ARG, "file_offsets[0] must be 0");
+    for (int i = 0; i < n; i++)
+        if (foff[i + 1] < foff[i]) return set_err(PAC_E_ARG, "file_offsets must be non-decreasing");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t bytes = foff[n];
+    const uint8_t* d = blob;
+    if (!blob_is_device) {
+        if ((rc = c->wav_blob.ensure(bytes + 1))) return rc;
+        if (bytes) HIPCHK(hipMemcpyAsync(c->wav_blob.p, blob, bytes, hipMemcpyHostToDevice, s));
+        d = c->wav_blob.p;
+    }
+    if ((rc = c->wav_foff.ensure(n + 1)) || (rc = c->wav_info.ensure(n))) return rc;
+    HIPCHK(hipMemcpyAsync(c->wav_foff.p, foff, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_wav_scan, dim3((n + 63) / 64), dim3(64), 0, s, d, c->wav_foff.p, n, c->wav_info.p,
+                       (int)PAC_HALFN);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(info, c->wav_info.p, n * sizeof(pac_wav_info), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *dev = d;
+    return PAC_OK;
+}
+
+extern "C" int pac_wav_scan(pac_ctx* c, int32_t n_files, const uint8_t* blob, const int64_t* file_offsets,
+                            int32_t blob_is_device, pac_wav_info* info) {
+    const uint8_t* d;
+    return wav_scan_dev(c, n_files, blob, file_offsets, blob_is_device, &d, info);
+}
+
+extern "C" int pac_encode_wav(pac_ctx* c, const pac_params* p, int32_t n_files, const uint8_t* blob,
+                              const int64_t* file_offsets, int32_t blob_is_device, uint8_t* out,
+                              int64_t out_capacity, int32_t out_is_device, int64_t* stream_byte_offsets,
+                              pac_stream_state* states, pac_wav_info* info_out) {
+    int rc;
+    if ((rc = check_params(p))) return rc;
+    std::vector<pac_wav_info> info(n_files > 0 ? n_files : 1);
+    const uint8_t* d = nullptr;
+    if ((rc = wav_scan_dev(c, n_files, blob, file_offsets, blob_is_device, &d, info.data()))) return rc;
+    if (info_out) memcpy(info_out, info.data(), n_files * sizeof(pac_wav_info));
+    const int nch = p->n_channels;
+    std::vector<int64_t> fo(n_files + 1, 0), segb(n_files + 1, 0);
+    for (int i = 0; i < n_files; i++) {
+        if (info[i].status) return set_err(PAC_E_ARG, "file %d: %s", i, wav_status_msg(info[i].status));
+        if (info[i].sample_rate != p->sample_rate || info[i].n_channels != nch)
+            return set_err(PAC_E_ARG, "file %d: %d Hz x %d channels, the call is %d Hz x %d", i,
+                           info[i].sample_rate, info[i].n_channels, p->sample_rate, nch);
+        fo[i + 1] = fo[i] + info[i].frames;
+        segb[i + 1] = segb[i] + (info[i].frames * nch * 2 + PAC_WAV_SEG - 1) / PAC_WAV_SEG;
+    }
+    hipStream_t s = c->stream;
+    if ((rc = c->wav_pcm.ensure(fo[n_files] * nch * 2 + 2)) || (rc = c->wav_fo.ensure(n_files + 1)) ||
+        (rc = c->wav_segb.ensure(n_files + 1)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(c->wav_fo.p, fo.data(), (n_files + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->wav_segb.p, segb.data(), (n_files + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (segb[n_files] > 0) {
+        hipLaunchKernelGGL(k_wav_gather, dim3((unsigned)segb[n_files]), dim3(256), 0, s, d, c->wav_foff.p,
+                           c->wav_info.p, c->wav_fo.p, c->wav_segb.p, n_files, nch, c->wav_pcm.p);
+        HIPCHK(hipGetLastError());
+    }
+    return pac_encode_streams(c, p, n_files, reinterpret_cast<const int16_t*>(c->wav_pcm.p), fo.data(), 1, out,
+                              out_capacity, out_is_device, stream_byte_offsets, states);
+}
+
+extern "C" int pac_decode_wav(pac_ctx* c, const pac_params* p, int32_t n_streams, const uint8_t* data,
+                              const int64_t* stream_byte_offsets, int32_t data_is_device,
+                              const int64_t* num_samples, uint8_t* out, int64_t out_capacity, int32_t out_is_device,
+                              int64_t* wav_offsets) {
+    int rc;
+    if (!c || !p || !data || !stream_byte_offsets || !num_samples || !wav_offsets || n_streams < 1)
+        return set_err(PAC_E_ARG, "null argument or n_streams < 1");
+    if ((rc = check_params(p))) return rc;
+    const int nch = p->n_channels;
+    std::vector<int64_t> fo(n_streams + 1, 0), segb(n_streams + 1, 0);
+    if (data_is_device) {           // frame offsets from the device data: size query
+        rc = pac_decode_streams(c, p, n_streams, data, stream_byte_offsets, 1, 0, nullptr, 0, 1, nullptr, fo.data());
+        if (rc != PAC_OK && rc != PAC_E_CAPACITY) return rc;
+    } else if ((rc = pac_decode_layout(p, n_streams, data, stream_byte_offsets, 0, fo.data()))) {
+        return rc;
+    }
+    const int64_t frames = fo[n_streams];
+    if ((rc = c->wav_pcm.ensure(frames * nch * 2 + 2))) return rc;
+    if ((rc = pac_decode_streams(c, p, n_streams, data, stream_byte_offsets, data_is_device, 0,
+                                 reinterpret_cast<int16_t*>(c->wav_pcm.p), frames, 1, nullptr, fo.data())))
+        return rc;
+    wav_offsets[0] = 0;
+    for (int k = 0; k < n_streams; k++) {
+        wav_offsets[k + 1] = wav_offsets[k] + 44 + (fo[k + 1] - fo[k]) * nch * 2;
+        segb[k + 1] = segb[k] + (44 + (fo[k + 1] - fo[k]) * nch * 2 + PAC_WAV_SEG - 1) / PAC_WAV_SEG;
+    }
+    const int64_t total = wav_offsets[n_streams];
+    if (total > out_capacity)
+        return set_err(PAC_E_CAPACITY, "WAV output needs %lld bytes, capacity %lld", (long long)total,
+                       (long long)out_capacity);
+    hipStream_t s = c->stream;
+    if ((rc = c->wav_fo.ensure(n_streams + 1)) || (rc = c->wav_segb.ensure(n_streams + 1)) ||
+        (rc = c->wav_ns.ensure(n_streams)) || (rc = c->wav_wo.ensure(n_streams + 1)))
+        return rc;
+    uint8_t* od = out;
+    if (!out_is_device) {
+        if ((rc = c->wav_out.ensure(total + 1))) return rc;
+        od = c->wav_out.p;
+    }
+    HIPCHK(hipMemcpyAsync(c->wav_fo.p, fo.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->wav_segb.p, segb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->wav_ns.p, num_samples, n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->wav_wo.p, wav_offsets, (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_wav_write, dim3((unsigned)segb[n_streams]), dim3(256), 0, s, c->wav_pcm.p, c->wav_fo.p,
+                       c->wav_ns.p, c->wav_wo.p, c->wav_segb.p, n_streams, nch, p->sample_rate, od);
+    HIPCHK(hipGetLastError());
+    if (!out_is_device) HIPCHK(hipMemcpyAsync(out, od, total, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return PAC_OK;
 }

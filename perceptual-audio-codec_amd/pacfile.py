@@ -178,6 +178,31 @@ def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):
     return data
 
 
+def encode_wav_files(wav_files, profile=PROFILE_MASTER, context=None, n_channels=None, sample_rate=None):
+    """The encode driver (pacfile.py:430-499) for many WAV files (paths or
+    bytes) sharing sample rate and channel count, with the WAV parsing on the
+    device (pac_encode_wav).  Returns the coded files' bytes."""
+    ctx = context or codec.default_context()
+    blobs = []
+    for w in wav_files:
+        if isinstance(w, (bytes, bytearray)):
+            blobs.append(bytes(w))
+        else:
+            with open(w, "rb") as f:
+                blobs.append(f.read())
+    fo = np.zeros(len(blobs) + 1, dtype=np.int64)
+    fo[1:] = np.cumsum([len(b) for b in blobs])
+    blob = b"".join(blobs)
+    if sample_rate is None or n_channels is None:
+        first = ctx.wav_scan(blobs[0], [0, len(blobs[0])])[0]
+        sample_rate = sample_rate or first.sample_rate
+        n_channels = n_channels or first.n_channels
+    p = _lib.params(sample_rate, n_channels, profile)
+    out, so, info = ctx.encode_wav(p, blob, fo)
+    return [header_bytes(w.sample_rate, w.n_channels, w.num_samples) + out[so[i]:so[i + 1]].tobytes()
+            for i, w in enumerate(info)]
+
+
 # ---------------------------------------------------------------------------
 # decoding (pacfile.py:153-229, codec.py:25-65, the driver pacfile.py:478-499)
 # ---------------------------------------------------------------------------
@@ -227,3 +252,18 @@ def decode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None):
         with open(out_path, "wb") as f:
             f.write(out)
     return out
+
+
+def decode_to_wav(coded_files, profile=PROFILE_MASTER, context=None):
+    """The decode driver (pacfile.py:430-499) for many coded files (bytes)
+    sharing sample rate and channel count: the output WAV files' bytes, the
+    WAV header and sample conversion written on the device (pac_decode_wav)."""
+    ctx = context or codec.default_context()
+    heads = [parse_header(b) for b in coded_files]
+    fs, nch = heads[0][0], heads[0][1]
+    secs = [b[h[4]:] for b, h in zip(coded_files, heads)]
+    so = np.zeros(len(secs) + 1, dtype=np.int64)
+    so[1:] = np.cumsum([len(x) for x in secs])
+    p = _lib.params(fs, nch, profile)
+    out, wo = ctx.decode_wav(p, b"".join(secs), so, [h[2] for h in heads])
+    return [out[wo[i]:wo[i + 1]].tobytes() for i in range(len(secs))]

@@ -251,6 +251,50 @@ class Job:
         self.ctx.free(self.out_dev)
         self.ctx.free(self.pcm_dev)
 
+    def cpu_samples(self, nt, max_frames=4096 * 1024):
+        """int16 frames of the first nt streams (copied back from HBM)"""
+        out = []
+        for t in range(min(nt, self.ns)):
+            n = min(int(self.fo[t + 1] - self.fo[t]), max_frames)
+            pcm = np.empty((n, 2), dtype=np.int16)
+            self.ctx.to_host(pcm, self.pcm_dev + int(self.fo[t]) * 4)
+            out.append(pcm)
+        return out
+
+
+class WavJob(Job):
+    """config 3: WAV files (raw bytes, back to back) resident in HBM; one step
+    = pac_encode_wav: the header scan, the frame gather and the encoder, all
+    on the device (the reference driver's whole encode half)."""
+
+    def __init__(self, ctx, p, blobs, frames_host):
+        self.ctx, self.p = ctx, p
+        self.ns = len(blobs)
+        self.foff = np.zeros(self.ns + 1, dtype=np.int64)
+        self.foff[1:] = np.cumsum([len(b) for b in blobs])
+        self.blob_dev = ctx.alloc(int(self.foff[-1]) + 8)
+        for j, b in enumerate(blobs):        # upload file by file (no host copy of the whole batch)
+            ctx.to_device(self.blob_dev + int(self.foff[j]), np.frombuffer(b, dtype=np.uint8))
+        info = ctx.wav_scan(self.blob_dev, self.foff, blob_is_device=True)
+        self.blocks = int(sum(shard.blocks_of(w.frames) for w in info))
+        self.frames_host = frames_host
+        self.cap = self.blocks * p.n_channels * 1024
+        self.out_dev = ctx.alloc(self.cap)
+        self.so = None
+        self.pcm_dev = None
+
+    def run(self):
+        _, self.so, _ = self.ctx.encode_wav(self.p, self.blob_dev, self.foff, blob_is_device=True, out=self.out_dev,
+                                            out_capacity=self.cap, out_is_device=True)
+        return self.ctx.last_timing()
+
+    def free(self):
+        self.ctx.free(self.out_dev)
+        self.ctx.free(self.blob_dev)
+
+    def cpu_samples(self, nt, max_frames=4096 * 1024):
+        return [fr[:max_frames] for fr in self.frames_host[:nt]]
+
 
 def synthetic_job(a, ctx, rank):
     fs = a.sample_rate
@@ -267,32 +311,28 @@ def synthetic_job(a, ctx, rank):
 
 
 def file_jobs(a, ctx, rank, world):
-    """config 3: stereo inputs x copies, this rank's LPT shard, one job per
-    sample rate.  Returns (jobs, description)."""
+    """config 3: the stereo inputs x copies as independent streams, this
+    rank's LPT shard (pac_amd.shard.plan), one WavJob per sample rate: the raw
+    WAV files go to HBM, the parsing happens in the timed step on the device."""
     from pac_amd.pcmfile import read_for_encode
     paths = sorted(glob.glob(os.path.join(INPUTS, "*.wav")))
-    reads = [(os.path.basename(pth), *read_for_encode(pth)) for pth in paths]
-    stereo = [(n, cp, fr) for n, cp, fr in reads if cp.nChannels == 2]
+    reads = [(os.path.basename(pth), pth, *read_for_encode(pth)) for pth in paths]
+    stereo = [r for r in reads if r[2].nChannels == 2]
     streams = [(i, c) for i in range(len(stereo)) for c in range(a.copies)]
-    counts = [shard.blocks_of(stereo[i][2].shape[0]) for i, _ in streams]
+    counts = [shard.blocks_of(stereo[i][3].shape[0]) for i, _ in streams]
     mine = shard.plan(counts, world)[rank]
     by_fs = {}
     for k in mine:
         i, _ = streams[k]
-        by_fs.setdefault(stereo[i][1].sampleRate, []).append(i)
+        by_fs.setdefault(stereo[i][2].sampleRate, []).append(i)
+    raw = [open(r[1], "rb").read() for r in stereo]
     jobs = []
     for fs, files in sorted(by_fs.items()):
-        lens = np.array([stereo[i][2].shape[0] for i in files], dtype=np.int64)
-        fo = np.zeros(len(files) + 1, dtype=np.int64)
-        fo[1:] = np.cumsum(lens)
-        pcm_dev = ctx.alloc(max(int(fo[-1]) * 4, 4))
-        # upload file by file (no host copy of the whole tiled batch)
-        for j, i in enumerate(files):
-            ctx.to_device(pcm_dev + int(fo[j]) * 4, stereo[i][2])
-        jobs.append(Job(ctx, _lib.params(fs, 2, 1), fo, pcm_dev))
-    desc = {"inputs": ["%s (%d Hz, %d frames)" % (n, cp.sampleRate, fr.shape[0]) for n, cp, fr in stereo],
-            "skipped_mono": [n for n, cp, _ in reads if cp.nChannels != 2],
-            "copies": a.copies, "streams_total": len(streams), "streams_this_rank": len(mine)}
+        jobs.append(WavJob(ctx, _lib.params(fs, 2, 1), [raw[i] for i in files], [stereo[i][3] for i in files]))
+    desc = {"inputs": ["%s (%d Hz, %d frames)" % (n, cp.sampleRate, fr.shape[0]) for n, _, cp, fr in stereo],
+            "skipped_mono": [n for n, _, cp, _ in reads if cp.nChannels != 2],
+            "copies": a.copies, "streams_total": len(streams), "streams_this_rank": len(mine),
+            "ingest": "raw WAV bytes in HBM; header scan + frame gather + encode per step (pac_encode_wav)"}
     return jobs, desc, stereo
 
 
@@ -526,14 +566,8 @@ def main():
         # the CPU sample: the first streams of the (first) job, copied back from HBM
         j = jobs[0]
         nt = max(1, min(a.cpu_threads, j.ns))
-        samples, starts = [], []
-        for t in range(nt):
-            n = int(j.fo[t + 1] - j.fo[t])
-            n = min(n, 4096 * 1024)
-            pcm = np.empty((n, 2), dtype=np.int16)
-            ctx.to_host(pcm, j.pcm_dev + int(j.fo[t]) * 4)
-            samples.append(pcm)
-            starts.append(int(j.so[t]))
+        samples = j.cpu_samples(nt)
+        starts = [int(j.so[t]) for t in range(len(samples))]
         res["cpu_baseline"], prefixes = cpu_baseline(ctx, samples, j.p.sample_rate, a.cpu_seconds, a.profile, nt)
         res["parity"] = parity_check(ctx, j.out_dev, starts, prefixes)
     for j in jobs:

@@ -46,8 +46,14 @@ typedef struct {
     int32_t n_table_id_bits;        /* codingParams.nTableIDBits (4, master)   */
     double target_bits_per_sample;  /* codingParams.targetBitsPerSample (2.27) */
     int32_t profile;                /* PAC_PROFILE_*                           */
-    int32_t reserved;
+    int32_t window;                 /* PAC_WINDOW_SINE (the reference), or
+                                       PAC_WINDOW_KBD: KBDWindow alpha 4
+                                       (window.py:56-78) as the MDCT window of
+                                       encoder and decoder -- an extension no
+                                       reference coder uses (parity unpinned) */
 } pac_params;
+#define PAC_WINDOW_SINE 0
+#define PAC_WINDOW_KBD 1
 
 /* Cross-block encoder state of one stream, so that a stream can be encoded
  * across calls (streaming, or an origin stream split over GPUs with a one-hop

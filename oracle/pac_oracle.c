@@ -120,6 +120,43 @@ static void assign_lines(int nlines_total, int fs, int *out) {
     }
 }
 
+/* KBDWindow (window.py:56-78), alpha 4, in long double (I0 by its power
+ * series), rounded once -- the same evaluation as the library's table, so the
+ * KBD extension (parity unpinned: no reference coder uses it) can be checked
+ * byte for byte between the HIP path and this restatement. */
+static long double bessel_i0l(long double x) {
+    long double sum = 1.0L, term = 1.0L;
+    const long double q = x * x / 4.0L;
+    for (int k = 1; k < 500; k++) {
+        term *= q / ((long double)k * (long double)k);
+        sum += term;
+        if (term < sum * 1e-22L) break;
+    }
+    return sum;
+}
+
+void pac_oracle_set_window(pac_oracle *t, int kind) {
+    if (kind == 1) {
+        long double k2[N / 2 + 1], den = 0.0L, cum = 0.0L;
+        const long double pa = (long double)M_PI * 4.0L, norm = bessel_i0l(pa);
+        for (int i = 0; i <= N / 2; i++) {
+            const long double r = 4.0L * i / N - 1.0L;
+            const long double kv = bessel_i0l(pa * sqrtl(fmaxl(0.0L, 1.0L - r * r))) / norm;
+            k2[i] = kv * kv;
+            den += k2[i];
+        }
+        for (int i = 0; i < N / 2; i++) {
+            cum += k2[i];
+            t->sine[i] = (double)sqrtl(cum / den);
+            t->sine[N - 1 - i] = t->sine[i];
+        }
+    } else {
+        for (int n = 0; n < N; n++) t->sine[n] = sin(((double)n + 0.5) * M_PI / (double)N);
+    }
+}
+
+double pac_oracle_window(const pac_oracle *t, int n) { return t->sine[n]; }
+
 pac_oracle *pac_oracle_create(int fs) {
     if (fs <= 0) return NULL;
     pac_oracle *t = (pac_oracle *)calloc(1, sizeof(pac_oracle));

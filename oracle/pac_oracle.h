@@ -49,6 +49,9 @@ typedef struct {            /* one stereo block, master profile */
 extern "C" {
 #endif
 pac_oracle *pac_oracle_create(int sample_rate);
+/* MDCT window: 0 SineWindow (the reference coders), 1 KBDWindow alpha 4 (extension) */
+void pac_oracle_set_window(pac_oracle *o, int kind);
+double pac_oracle_window(const pac_oracle *o, int n);
 void pac_oracle_destroy(pac_oracle *t);
 int pac_oracle_nlines(const pac_oracle *t, int *out25);
 int pac_oracle_load_huffman(pac_oracle *t, const uint8_t *buf, int64_t len);

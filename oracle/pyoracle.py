@@ -67,6 +67,9 @@ def lib():
         L.pac_oracle_imdct_window.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.pac_oracle_float_to_pcm.restype = C.c_int16
         L.pac_oracle_float_to_pcm.argtypes = [C.c_double]
+        L.pac_oracle_set_window.argtypes = [C.c_void_p, C.c_int]
+        L.pac_oracle_window.restype = C.c_double
+        L.pac_oracle_window.argtypes = [C.c_void_p, C.c_int]
         L.pac_oracle_encode.restype = C.c_int64
         L.pac_oracle_encode.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int,
                                         C.c_int64, C.c_void_p, C.c_int64, C.POINTER(State)]
@@ -75,11 +78,13 @@ def lib():
 
 
 class Oracle:
-    def __init__(self, sample_rate, huffman=True):
+    def __init__(self, sample_rate, huffman=True, window=0):
         self.L = lib()
         self.h = self.L.pac_oracle_create(int(sample_rate))
         if not self.h:
             raise ValueError("bad sample rate")
+        if window:
+            self.L.pac_oracle_set_window(self.h, int(window))
         if huffman:
             with open(HUFF, "rb") as f:
                 buf = f.read()
@@ -93,6 +98,9 @@ class Oracle:
             self.L.pac_oracle_destroy(self.h)
         except Exception:
             pass
+
+    def window(self):
+        return np.array([self.L.pac_oracle_window(self.h, n) for n in range(2048)])
 
     def nlines(self):
         out = (C.c_int * 25)()

@@ -28,7 +28,11 @@ class Params(C.Structure):
                 ("n_mdct_lines", C.c_int32), ("n_scale_bits", C.c_int32),
                 ("n_mant_size_bits", C.c_int32), ("n_table_id_bits", C.c_int32),
                 ("target_bits_per_sample", C.c_double), ("profile", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("window", C.c_int32)]
+
+
+WINDOW_SINE = 0      # SineWindow (window.py:27-39): the reference coders
+WINDOW_KBD = 1       # KBDWindow alpha 4 (window.py:56-78): extension, parity unpinned
 
 
 STREAM_HAS_PRIOR = 1     # include/pac_gpu.h: first 1024 frames are the priorBlock
@@ -359,7 +363,7 @@ class Context:
         return t
 
 
-def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27):
+def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27, window=WINDOW_SINE):
     p = Params()
     p.sample_rate = int(sample_rate)
     p.n_channels = int(n_channels)
@@ -369,4 +373,5 @@ def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27):
     p.n_table_id_bits = 4
     p.target_bits_per_sample = float(target_bits_per_sample)
     p.profile = int(profile)
+    p.window = int(window)
     return p

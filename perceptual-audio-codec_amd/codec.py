@@ -29,7 +29,8 @@ def default_context():
 
 def _params_from(codingParams, profile):
     p = _lib.params(codingParams.sampleRate, codingParams.nChannels, profile,
-                    getattr(codingParams, "targetBitsPerSample", 2.27))
+                    getattr(codingParams, "targetBitsPerSample", 2.27),
+                    window=getattr(codingParams, "window", _lib.WINDOW_SINE))   # KBD: extension
     p.n_mdct_lines = int(codingParams.nMDCTLines)
     p.n_scale_bits = int(codingParams.nScaleBits)
     p.n_mant_size_bits = int(codingParams.nMantSizeBits)

@@ -87,7 +87,40 @@ static void host_band_layout(int fs, int32_t* out) {
     }
 }
 
-static void build_tables(int fs, PacTables* t) {
+// KBDWindow (window.py:56-78), alpha = 4: the Kaiser kernel over t = 0..N/2,
+// w[n] = sqrt(cumsum(kaiser[:-1]^2)[n] / sum(kaiser^2)), mirrored.  Evaluated
+// in long double (I0 by its power series) and rounded once: Princen-Bradley
+// w[n]^2 + w[n+N/2]^2 = 1 holds to the last bit of the rounding.
+static long double bessel_i0(long double x) {
+    long double sum = 1.0L, term = 1.0L;
+    const long double q = x * x / 4.0L;
+    for (int k = 1; k < 500; k++) {
+        term *= q / ((long double)k * (long double)k);
+        sum += term;
+        if (term < sum * 1e-22L) break;
+    }
+    return sum;
+}
+static void kbd_window(int n, double alpha, double* w) {
+    const int h = n / 2;
+    std::vector<long double> k2(h + 1);
+    const long double pa = (long double)M_PI * (long double)alpha, norm = bessel_i0(pa);
+    long double den = 0.0L;
+    for (int t = 0; t <= h; t++) {
+        const long double r = 4.0L * t / n - 1.0L;
+        const long double kv = bessel_i0(pa * sqrtl(fmaxl(0.0L, 1.0L - r * r))) / norm;
+        k2[t] = kv * kv;
+        den += k2[t];
+    }
+    long double cum = 0.0L;
+    for (int t = 0; t < h; t++) {
+        cum += k2[t];
+        w[t] = (double)sqrtl(cum / den);
+        w[n - 1 - t] = w[t];
+    }
+}
+
+static void build_tables(int fs, int window, PacTables* t) {
     memset(t, 0, sizeof(*t));
     t->sample_rate = fs;
     host_band_layout(fs, t->nlines);
@@ -103,6 +136,7 @@ static void build_tables(int fs, PacTables* t) {
         t->sine[n] = sin((tt + 0.5) * M_PI / (double)PAC_N);
         t->hann[n] = 0.5 * (1 - cos(2.0 * (tt + 0.5) * M_PI / (double)PAC_N));
     }
+    if (window == PAC_WINDOW_KBD) kbd_window(PAC_N, 4.0, t->sine);   // the MDCT window of every kernel
     const double M = PAC_HALFN;
     for (int q = 0; q < PAC_HALFN / 2; q++) {
         double a = -M_PI * (q + 0.25) / M;
@@ -336,15 +370,16 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     delete c;
 }
 
-static int get_tables(pac_ctx* c, int fs, PacTables** out) {
-    auto it = c->tables.find(fs);
+static int get_tables(pac_ctx* c, int fs, int window, PacTables** out) {
+    const int key = fs * 4 + window;
+    auto it = c->tables.find(key);
     if (it != c->tables.end()) {
         *out = it->second;
         return PAC_OK;
     }
     PacTables* h = (PacTables*)malloc(sizeof(PacTables));
     if (!h) return set_err(PAC_E_NOMEM, "host tables");
-    build_tables(fs, h);
+    build_tables(fs, window, h);
     if (h->lr_nleaf > 64) {
         free(h);
         return set_err(PAC_E_UNSUPPORTED, "band layout of %d Hz needs more than 64 pairwise-sum leaves", fs);
@@ -357,7 +392,7 @@ static int get_tables(pac_ctx* c, int fs, PacTables** out) {
     hipError_t e = hipMemcpy(d, h, sizeof(PacTables), hipMemcpyHostToDevice);
     free(h);
     if (e != hipSuccess) return set_err(PAC_E_HIP, "table upload: %s", hipGetErrorString(e));
-    c->tables[fs] = d;
+    c->tables[key] = d;
     *out = d;
     return PAC_OK;
 }
@@ -484,6 +519,7 @@ static int check_params(const pac_params* p) {
         return set_err(PAC_E_ARG, "unknown profile %d", p->profile);
     }
     if (!(p->target_bits_per_sample > 0.0)) return set_err(PAC_E_ARG, "targetBitsPerSample");
+    if (p->window != PAC_WINDOW_SINE && p->window != PAC_WINDOW_KBD) return set_err(PAC_E_ARG, "window %d", p->window);
     return PAC_OK;
 }
 
@@ -794,7 +830,7 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
             return set_err(PAC_E_ARG, "frame_offsets must be non-decreasing");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
-    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    if ((rc = get_tables(c, p->sample_rate, p->window, &T))) return rc;
     const int nch = p->n_channels;
     // blocks per stream: every hop after the (optional) carried priorBlock, plus
     // the Close() flush block unless the stream continues in a later call
@@ -910,7 +946,7 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
     if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
-    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    if ((rc = get_tables(c, p->sample_rate, p->window, &T))) return rc;
     const int nch = p->n_channels;
     const int64_t G = nch;
     hipStream_t s = c->stream;
@@ -1069,7 +1105,7 @@ extern "C" int pac_debug_threshold(pac_ctx* c, int32_t sample_rate, int32_t n, c
     if (!c || !data || !thr || !npeaks || n < 1) return set_err(PAC_E_ARG, "bad argument");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
-    if ((rc = get_tables(c, sample_rate, &T))) return rc;
+    if ((rc = get_tables(c, sample_rate, PAC_WINDOW_SINE, &T))) return rc;
     double *dd = nullptr, *dt = nullptr;
     int32_t* dp = nullptr;
     HIPCHK(hipMalloc((void**)&dd, (size_t)n * PAC_N * sizeof(double)));
@@ -1090,7 +1126,7 @@ extern "C" int pac_debug_mdct(pac_ctx* c, int32_t n, const double* data, double*
     int rc;
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
-    if ((rc = get_tables(c, 48000, &T))) return rc;
+    if ((rc = get_tables(c, 48000, PAC_WINDOW_SINE, &T))) return rc;
     double *dd = nullptr, *dx = nullptr;
     HIPCHK(hipMalloc((void**)&dd, (size_t)n * PAC_N * sizeof(double)));
     HIPCHK(hipMalloc((void**)&dx, (size_t)n * PAC_HALFN * sizeof(double)));
@@ -1163,7 +1199,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
             return set_err(PAC_E_ARG, "stream_byte_offsets must be non-decreasing");
     HIPCHK(hipSetDevice(c->device));
     PacTables* T;
-    if ((rc = get_tables(c, p->sample_rate, &T))) return rc;
+    if ((rc = get_tables(c, p->sample_rate, p->window, &T))) return rc;
     hipStream_t s = c->stream;
     const int64_t nbytes = stream_byte_offsets[n_streams];
     const uint8_t* ddev = data;

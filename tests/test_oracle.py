@@ -175,3 +175,18 @@ def test_manifest_hashes():
     for fn, h in m["files"].items():
         with open(os.path.join(GOLD, fn), "rb") as f:
             assert hashlib.sha256(f.read()).hexdigest() == h, fn
+
+
+def test_kbd_window_matches_window_py():
+    """the oracle's KBD window (extension) against a numpy restatement of
+    window.py:56-78 (alpha 4, np.i0), and Princen-Bradley"""
+    o = P.Oracle(48000, window=1)
+    w = o.window()
+    N = 2048.
+    t = np.arange(int(N / 2 + 1))
+    kaiser = np.i0(4. * np.pi * np.sqrt(1.0 - (4.0 * t / N - 1.0) ** 2)) / np.i0(np.pi * 4.)
+    num = np.cumsum(kaiser[:-1] ** 2)
+    ref = np.sqrt(np.concatenate((num, num[::-1])) / np.sum(kaiser ** 2))
+    assert np.max(np.abs(w - ref)) < 4e-15
+    assert np.max(np.abs(w[:1024] ** 2 + w[1024:] ** 2 - 1.0)) < 5e-16
+    assert np.array_equal(P.Oracle(48000).window(), np.sin((np.arange(2048) + 0.5) * np.pi / 2048))

@@ -39,7 +39,7 @@ typedef struct pac_ctx pac_ctx;
  * (pacfile.py:452-461 / Origin pacfile.py:391-398). */
 typedef struct {
     int32_t sample_rate;            /* codingParams.sampleRate                 */
-    int32_t n_channels;             /* codingParams.nChannels (master: 2)      */
+    int32_t n_channels;             /* nChannels (master: 2; 1 = mono ext.)    */
     int32_t n_mdct_lines;           /* codingParams.nMDCTLines (1024)          */
     int32_t n_scale_bits;           /* codingParams.nScaleBits (4)             */
     int32_t n_mant_size_bits;       /* codingParams.nMantSizeBits (4)          */

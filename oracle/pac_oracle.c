@@ -628,11 +628,15 @@ static long withdraw(long *deposit) {
 
 /* codec.Encode + EncodeDualChannel (codec.py:83-129, 212-281) and
  * getStereoMaskThreshold (psychoac.py:506-682).  xL/xR: 2048 raw samples,
- * modified in place like the reference. */
+ * modified in place like the reference.  xR == NULL: the mono master
+ * extension (not in the reference, parity unpinned) -- LRMS all 0, channel 0
+ * alone: BTHR_L, its SMRs, one BitAlloc + Huffman + deposit per block. */
 void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
                              pac_oracle_state *st, pac_oracle_stblock *o) {
+    const int nch = xR ? 2 : 1;
+    memset(o->lrms, 0, sizeof(o->lrms));
     /* LRMS decision on the raw (unwindowed) blocks codec.py:94-102 */
-    {
+    if (nch == 2) {
         double Lr[N], Li[N], Rr[N], Ri[N];
         for (int n = 0; n < N; n++) { Lr[n] = xL[n]; Li[n] = 0; Rr[n] = xR[n]; Ri[n] = 0; }
         fft2048(t, Lr, Li);
@@ -665,7 +669,12 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
 
     double XL[HALFN], XR[HALFN];
     mdct_and_scale(t, xL, XL, &o->overall[0], o->mdct[0]);
-    mdct_and_scale(t, xR, XR, &o->overall[1], o->mdct[1]);
+    if (nch == 2) {
+        mdct_and_scale(t, xR, XR, &o->overall[1], o->mdct[1]);
+    } else {
+        memset(XR, 0, sizeof(XR));
+        o->overall[1] = 0;
+    }
 
     /* getStereoMaskThreshold */
     double splL[HALFN], splR[HALFN], splM[HALFN], splS[HALFN];
@@ -680,6 +689,18 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
         splS[k] = SPL(4. * (S[k] * S[k])) - gR;
     }
     o->npeaks[0] = pac_oracle_threshold(t, xL, 0, o->bthr[0], NULL);   /* BTHR_L */
+    if (nch == 1) {
+        for (int b = 0; b < NB; b++) {
+            double lr0 = -INFINITY;
+            for (int l = t->lower[b]; l <= t->upper[b]; l++) {
+                const double v = splL[l] - o->bthr[0][l];
+                if (v > lr0) lr0 = v;
+                o->lines[0][l] = XL[l];
+            }
+            o->smr[0][b] = t->nlines[b] == 0 ? -96.0 : lr0;
+        }
+        goto alloc;
+    }
     o->npeaks[1] = pac_oracle_threshold(t, xR, 0, o->bthr[1], NULL);   /* BTHR_R */
     double dM[N], dS[N];
     for (int n = 0; n < N; n++) {
@@ -716,7 +737,8 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
             o->lines[1][l] = o->lrms[b] ? S[l] : XR[l];
         }
     }
-    for (int ch = 0; ch < 2; ch++) {
+alloc:
+    for (int ch = 0; ch < nch; ch++) {
         long diff = bitalloc_master(t, bitBudget, st->extraBits, 16, o->smr[ch], o->lrms,
                                     o->ba[ch]);
         st->extraBits += diff;
@@ -724,7 +746,7 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
     }
     o->extra_out = st->extraBits;
     /* Huffman per channel, then deposit (codec.py:111-124) */
-    for (int ch = 0; ch < 2; ch++) {
+    for (int ch = 0; ch < nch; ch++) {
         long hbits = 0;
         o->table_id[ch] = t->have_huff ? huffman_choose(t, o->ba[ch], o->mant[ch], &hbits) : 0;
         long origin = 0, nsign = 0;
@@ -906,7 +928,7 @@ static void parse_chblock(const pac_oracle *t, int profile, const uint8_t *p, in
 int64_t pac_oracle_decode(const pac_oracle *t, int profile, const uint8_t *data, int64_t nbytes, int n_ch,
                           int16_t *pcm, double *fout, int64_t max_frames) {
     if (n_ch < 1 || n_ch > 8) return -1;
-    if (profile == PAC_ORACLE_MASTER && (n_ch != 2 || !t->have_huff)) return -1;
+    if (profile == PAC_ORACLE_MASTER && (n_ch > 2 || !t->have_huff)) return -1;
     double *prev = (double *)calloc((size_t)n_ch * HALFN, sizeof(double));
     double *lines = (double *)malloc((size_t)n_ch * HALFN * sizeof(double));
     double *y = (double *)malloc((size_t)n_ch * N * sizeof(double));
@@ -936,7 +958,7 @@ int64_t pac_oracle_decode(const pac_oracle *t, int profile, const uint8_t *data,
                 const double rescale = 1. * (double)(1 << overall);
                 for (int l = 0; l < HALFN; l++) L[l] /= rescale;
             }
-            if (profile == PAC_ORACLE_MASTER) {
+            if (profile == PAC_ORACLE_MASTER && n_ch == 2) {
                 /* codec.py:46-54.  mdctLineL/R ALIAS mdctLine[0]/[1], so the
                  * second assignment reads the already-updated channel 0:
                  * L = M - S, R = (M - S) + S */
@@ -983,7 +1005,7 @@ done:
 int64_t pac_oracle_encode(const pac_oracle *t, int profile, const int16_t *pcm,
                           int64_t n_frames, int n_ch, int64_t max_blocks,
                           uint8_t *out, int64_t cap, pac_oracle_state *state) {
-    if (profile == PAC_ORACLE_MASTER && (n_ch != 2 || !t->have_huff)) return -1;
+    if (profile == PAC_ORACLE_MASTER && (n_ch > 2 || !t->have_huff)) return -1;   /* 1: mono extension */
     if (n_ch < 1 || n_ch > 8) return -1;
     int64_t hops = (n_frames + HALFN - 1) / HALFN;
     int64_t nblocks = hops + 1;                     /* + Close() flush block */
@@ -1014,8 +1036,8 @@ int64_t pac_oracle_encode(const pac_oracle *t, int profile, const int16_t *pcm,
                 pos += emit_origin(t, co, out + pos);
             }
         } else {
-            pac_oracle_block_master(t, full, full + N, st, so);
-            for (int c = 0; c < 2; c++) pos += emit_master(t, so, c, out + pos);
+            pac_oracle_block_master(t, full, n_ch == 2 ? full + N : NULL, st, so);
+            for (int c = 0; c < n_ch; c++) pos += emit_master(t, so, c, out + pos);
         }
     }
     ret = pos;

@@ -128,11 +128,12 @@ class Oracle:
         return o
 
     def block_master(self, xL, xR, state):
+        """xR None: the mono master extension (channel 0 alone, LRMS 0)"""
         a = np.array(xL, dtype=np.float64)
-        b = np.array(xR, dtype=np.float64)
+        b = None if xR is None else np.array(xR, dtype=np.float64)
         o = StBlock()
-        self.L.pac_oracle_block_master(self.h, a.ctypes.data, b.ctypes.data, C.byref(state),
-                                       C.byref(o))
+        self.L.pac_oracle_block_master(self.h, a.ctypes.data, None if b is None else b.ctypes.data,
+                                       C.byref(state), C.byref(o))
         return o
 
     def encode_data(self, profile, pcm, max_blocks=-1, state=None):

@@ -512,8 +512,10 @@ static int check_params(const pac_params* p) {
     if (p->profile == PAC_PROFILE_ORIGIN) {
         if (p->n_channels < 1 || p->n_channels > 8) return set_err(PAC_E_ARG, "n_channels %d", p->n_channels);
     } else if (p->profile == PAC_PROFILE_MASTER) {
-        if (p->n_channels != 2)
-            return set_err(PAC_E_UNSUPPORTED, "master coder is stereo only (codec.py:46-47,98)");
+        // the reference's master coder is stereo only (codec.py:46-47,98); one
+        // channel is this build's extension (LRMS all 0, parity unpinned)
+        if (p->n_channels != 2 && p->n_channels != 1)
+            return set_err(PAC_E_UNSUPPORTED, "master coder: 1 or 2 channels (codec.py:46-47,98)");
         if (p->n_table_id_bits != 4) return set_err(PAC_E_UNSUPPORTED, "nTableIDBits must be 4");
     } else {
         return set_err(PAC_E_ARG, "unknown profile %d", p->profile);
@@ -698,7 +700,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     int rc;
     const int n_streams = src.n_streams;
     const int64_t nblocks = blk[n_streams];
-    const int64_t G = 2 * nblocks;
+    const int nch = src.n_ch;                          // 2, or 1 (mono master extension)
+    const int64_t G = nch * nblocks;
+    const int nvar = nch == 2 ? 6 : 1;                 // threshold variants per block
     const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : 1;
     // chunk geometry: group [g0, g1) of at most CB streams, S blocks each
     struct Grp { int g0, n_s, S; int64_t gmax; };
@@ -745,21 +749,24 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipEventRecord(e, k ? s1 : s0));
         return PAC_OK;
     };
+    // mono: the LRMS flags are all 0 (L/R coding; the 25 bits are still written)
+    if (nch == 1) HIPCHK(hipMemsetAsync(c->m_lrms.p, 0, nblocks * PAC_NB, s0));
     HIPCHK(hipEventRecord(c->evs[4], s0));            // states and tables are on s0
     HIPCHK(hipStreamWaitEvent(s1, c->evs[4], 0));
     int64_t i = 0;
     for (const Grp& gr : groups) {
         for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S, ++i) {
             const int k = (int)(i & 1);
-            const PacMasterChunk ck{gr.g0, gr.n_s, t0, gr.S};
+            const PacMasterChunk ck{gr.g0, gr.n_s, t0, gr.S, nch};
             const PacMasterChunkBuf K{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                       c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB};
             const int64_t B = (int64_t)gr.n_s * gr.S;
             if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
             if ((rc = mark(0, -1))) return rc;
-            hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
+            if (nch == 2)
+                hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
             if ((rc = mark(0, 5))) return rc;
-            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * 6)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
             if ((rc = mark(0, 0))) return rc;
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             HIPCHK(hipGetLastError());
@@ -971,14 +978,14 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
         if ((rc = run_master(c, p, T, src, blk, c->out_stage.p, c->out_stage.n, &total, fields != nullptr)))
             return rc;
         if (fields) {   // per-line mantissas and Huffman codes as the pack kernel emitted them
-            dbg_mant.resize(2 * PAC_HALFN);
-            dbg_code.resize(2 * PAC_HALFN);
-            dbg_len.resize(2 * PAC_HALFN);
-            HIPCHK(hipMemcpyAsync(dbg_mant.data(), c->dbg_mant.p, 2 * PAC_HALFN * sizeof(uint32_t),
+            dbg_mant.resize(G * PAC_HALFN);
+            dbg_code.resize(G * PAC_HALFN);
+            dbg_len.resize(G * PAC_HALFN);
+            HIPCHK(hipMemcpyAsync(dbg_mant.data(), c->dbg_mant.p, G * PAC_HALFN * sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(dbg_code.data(), c->dbg_code.p, 2 * PAC_HALFN * sizeof(uint64_t),
+            HIPCHK(hipMemcpyAsync(dbg_code.data(), c->dbg_code.p, G * PAC_HALFN * sizeof(uint64_t),
                                   hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(dbg_len.data(), c->dbg_len.p, 2 * PAC_HALFN, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(dbg_len.data(), c->dbg_len.p, G * PAC_HALFN, hipMemcpyDeviceToHost, s));
         }
         HIPCHK(hipMemcpyAsync(&ex, c->st_extra.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&dp, c->st_deposit.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1192,7 +1199,6 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     const bool master = p->profile == PAC_PROFILE_MASTER;
     const int nch = p->n_channels;
     if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
-    if (master && nch != 2) return set_err(PAC_E_UNSUPPORTED, "master profile is stereo");
     if (stream_byte_offsets[0] != 0) return set_err(PAC_E_ARG, "stream_byte_offsets[0] must be 0");
     for (int s = 0; s < n_streams; s++)
         if (stream_byte_offsets[s + 1] < stream_byte_offsets[s])

@@ -259,9 +259,10 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
     __shared__ double lines[2][PAC_HALFN];
     __shared__ double prev[2][PAC_HALFN];
     const int tid = threadIdx.x;
-    const int nc = master ? 2 : 1;
-    const int64_t item = blockIdx.x / (master ? 1 : nch);
-    const int c0 = master ? 0 : (int)(blockIdx.x % nch);
+    const bool pair = master && nch == 2;          // M/S stereo pair (mono master: per channel)
+    const int nc = pair ? 2 : 1;
+    const int64_t item = blockIdx.x / (pair ? 1 : nch);
+    const int c0 = pair ? 0 : (int)(blockIdx.x % nch);
     // stream of this segment: last s with seg_base[s] <= item
     int lo = 0, hi = n_streams;
     while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (seg_base[mid] <= item) lo = mid; else hi = mid; }
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
         for (int c = 0; c < nc; ++c)
             grp_dequant<256>(T, D, cb_base[s] + b * nch + c0 + c, lines[c], tid);
         __syncthreads();
-        if (master) {
+        if (pair) {
             // codec.py:46-54: mdctLineL/R alias mdctLine[0]/[1]; the second
             // assignment reads the updated channel 0: L = M - S, R = (M - S) + S
             const uint8_t* lr = D.lrms + (cb_base[s] + b * nch + 1) * PAC_NB;   // last channel's bits

@@ -33,7 +33,7 @@ struct PacMasterChunkBuf {
     double* bandpeak;   // [Bc][2][25]    max |line| per band
 };
 
-// per-call fields; channel-block g = 2 gb + ch (gb = global block, file order)
+// per-call fields; channel-block g = nch gb + ch (gb = global block, file order)
 struct PacMasterFields {
     uint8_t* lrms;      // [nblocks][25]
     uint8_t* overall;   // [G]
@@ -54,6 +54,7 @@ struct PacMasterChunk {
     int s_first, n_s;
     int64_t t0;
     int S;
+    int nch;        // 2, or 1 for the mono master extension (no LRMS, one threshold)
 };
 
 // global block id of local block j, false if that stream has ended
@@ -92,8 +93,9 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
-    const int64_t j = item / 6;                // block within the chunk
-    const int v = (int)(item % 6);
+    const int nvar = ck.nch == 2 ? 6 : 1;      // mono master: BTHR_L only
+    const int64_t j = item / nvar;             // block within the chunk
+    const int v = (int)(item % nvar);
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;     // uniform per workgroup
     // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int rows = rowmask;
     if (!rows) return;                                      // uniform per workgroup
     const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, 1));
+    const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
     const MaskerLists L = masker_lists(buf, tmp, rank);
@@ -272,21 +274,23 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     const int64_t j = blockIdx.x;
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    const bool st = ck.nch == 2;                 // mono master: channel 0 alone, LRMS all 0
     const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, 1));
+    const BlockPcm rR(locate(src, gb, st ? 1 : 0));
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     if (tid < PAC_NB) lrms_s[tid] = F.lrms[gb * PAC_NB + tid];
     __syncthreads();
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
     const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-    const double* XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
+    const double* XR = st ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
+                          : nullptr;
     double xl4[4], xr4[4];
     double mL = 0.0, mR = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         xl4[i] = XL[i * 256 + tid];
-        xr4[i] = XR[i * 256 + tid];
+        xr4[i] = st ? XR[i * 256 + tid] : 0.0;
         mL = fmax(mL, fabs(xl4[i]));
         mR = fmax(mR, fabs(xr4[i]));
     }
@@ -297,7 +301,10 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
     const double gL = (double)(1 << oL), gR = (double)(1 << oR);
     const double offL = 6.02 * oL, offR = 6.02 * oR;
-    if (tid == 0) { F.overall[gb * 2] = (uint8_t)oL; F.overall[gb * 2 + 1] = (uint8_t)oR; }
+    if (tid == 0) {
+        F.overall[gb * ck.nch] = (uint8_t)oL;
+        if (st) F.overall[gb * 2 + 1] = (uint8_t)oR;
+    }
 
     // --- per-line SMR terms (psychoac.py:533-597), selection (:662-682) ----
     const double* thr = K.thr + j * 6 * PAC_HALFN;
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
             d1 = (pac_spl(4. * (S * S)) - offR) - thrS;
         } else {
             d0 = (pac_spl(4. * (xl * xl)) - offL) - thr[0 * PAC_HALFN + l];
-            d1 = (pac_spl(4. * (xr * xr)) - offR) - thr[1 * PAC_HALFN + l];
+            d1 = st ? (pac_spl(4. * (xr * xr)) - offR) - thr[1 * PAC_HALFN + l] : 0.0;
         }
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;
@@ -450,6 +457,7 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
     const int lane = threadIdx.x;
     const int r = lane >> 4, q = lane & 15;
     const int sl = blockIdx.x * 4 + r;
+    const int nch = ck.nch;
     if (sl >= ck.n_s) return;                          // whole rows only
     const int s = ck.s_first + sl;
     const int64_t bb0 = blk_off[s];
@@ -470,8 +478,8 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
         else if (deposit < 0) { e = deposit; deposit = 0; }
         extra += e;
         long dep_add = 0;
-        for (int ch = 0; ch < 2; ++ch) {
-            const int64_t gl = j * 2 + ch, g = gb * 2 + ch;
+        for (int ch = 0; ch < nch; ++ch) {
+            const int64_t gl = j * 2 + ch, g = gb * nch + ch;
             int a0, a1;
             extra += bitalloc_master_row(K.smr + gl * PAC_NB, F.lrms + gb * PAC_NB, T, bitBudget, extra, 16, q,
                                          &a0, &a1);
@@ -582,18 +590,21 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
     const int c = w >> 1, h = w & 1;
+    const int nch = src.n_ch;                  // 2, or 1: mono master extension
     const int64_t gb = xcd_item(blockIdx.x, nblocks);
     const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, 1));
+    const BlockPcm rR(locate(src, gb, nch == 2 ? 1 : 0));
     if (tid < PAC_NB) lr[tid] = F.lrms[gb * PAC_NB + tid];
-    if (tid < 2 * PAC_NB) {
+    if (tid < nch * PAC_NB) {
         const int cc = tid / PAC_NB, b = tid % PAC_NB;
-        bas[cc][b] = F.ba[(gb * 2 + cc) * PAC_NB + b];
-        sfs[cc][b] = F.sf[(gb * 2 + cc) * PAC_NB + b];
+        bas[cc][b] = F.ba[(gb * nch + cc) * PAC_NB + b];
+        sfs[cc][b] = F.sf[(gb * nch + cc) * PAC_NB + b];
     }
     const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-    const double* XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
-    const double gL = (double)(1 << F.overall[gb * 2]), gR = (double)(1 << F.overall[gb * 2 + 1]);
+    const double* XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
+                                : XL;
+    const double gL = (double)(1 << F.overall[gb * nch]);
+    const double gR = nch == 2 ? (double)(1 << F.overall[gb * 2 + 1]) : gL;
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
     double* L0 = reinterpret_cast<double*>(bufA);
     double* L1 = reinterpret_cast<double*>(bufB);
@@ -604,10 +615,11 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
         const int ms = l < lend ? lr[T->band_of_line[l]] : 0;
         L0[l] = ms ? M : xl;
-        L1[l] = ms ? S : xr;
+        if (nch == 2) L1[l] = ms ? S : xr;
     }
     __syncthreads();
-    const int64_t g = gb * 2 + c;
+    const bool act = c < nch;                  // mono: waves 2, 3 only zero the words and meet the barriers
+    const int64_t g = gb * nch + (act ? c : 0);
     const int tb = F.tid[g] - 1;
     const double* ln = c ? L1 : L0;
     // this wave's 8 rows: sign + code of length clen per line (0 for ba == 0 bands)
@@ -620,7 +632,7 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         const int ba = bas[c][b];
         clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
         uint32_t m = 0;
-        if (ba) {
+        if (ba && act) {
             m = pac_mantissa(ln[l], sfs[c][b], ba);
             const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
             sgn[q] = (m >> (ba - 1)) & 1u;
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
             if (L) { clen[q] = L; code[q] = H->bits[tb][sym]; }
             else { clen[q] = H->esc_len[tb] + ba; esc[q] = 1; code[q] = sym; }
         }
-        if (F.dbg_code) {
+        if (F.dbg_code && act) {
             const int64_t i = g * PAC_HALFN + l;
             F.dbg_mant[i] = m;
             F.dbg_code[i] = esc[q] ? (((uint64_t)H->esc_bits[tb] << ba) | code[q]) : (uint64_t)code[q];
@@ -643,14 +655,15 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         pre[q] = run + wave_excl_scan_i(clen[q], &t);
         run += t;
     }
-    if (h == 0 && lane == 0) half_bits[c] = run;
+    if (act && h == 0 && lane == 0) half_bits[c] = run;
     __syncthreads();                  // every line read: bufA / bufB become the packed words
     uint32_t* wd = reinterpret_cast<uint32_t*>(c ? bufB : bufA);
     for (int i = tid; i < PACK_WORDS_MASTER; i += 256) {
         reinterpret_cast<uint32_t*>(bufA)[i] = 0u;
         reinterpret_cast<uint32_t*>(bufB)[i] = 0u;
     }
-    if (h) {
+    if (!act) {
+    } else if (h) {
         const int hoff = half_bits[c];
 #pragma unroll
         for (int q = 0; q < 8; ++q) pre[q] += hoff;
@@ -665,10 +678,11 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
     for (int q = 0; q < 8; ++q) {
         const int l = (8 * h + q) * WAVE + lane;
         const int b = T->band_of_line[l];
-        if (l == T->lower[b] && T->nlines[b]) pal[c][b] = pre[q];
+        if (act && l == T->lower[b] && T->nlines[b]) pal[c][b] = pre[q];
     }
     __syncthreads();
-    if (h == 0) {
+    if (!act) {
+    } else if (h == 0) {
         if (lane == 0) {
             put_bits(wd, 0, (uint32_t)F.overall[g], 4);
             put_bits(wd, 4, (uint32_t)(tb + 1), 4);
@@ -694,7 +708,7 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
     for (int q = 0; q < 8; ++q) {
         const int l = (8 * h + q) * WAVE + lane;
         const int b = T->band_of_line[l];
-        const int ba = bas[c][b];
+        const int ba = act ? bas[c][b] : 0;
         if (!ba) continue;
         const int p0 = bstart[c][b] + pal[c][b] + 8;
         put_bits(wd, p0 + (l - T->lower[b]), sgn[q], 1);
@@ -709,7 +723,7 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
     }
     __syncthreads();
     const int nb = F.nbytes[g];
-    if (off[g] + nb > cap) return;
+    if (!act || off[g] + nb > cap) return;
     uint8_t* o = out + off[g];
     if (h == 0 && lane < 4) o[lane] = (uint8_t)((uint32_t)(nb - 4) >> (8 * lane));   // '<L' nBytes
     for (int i = h * WAVE + lane; i < nb - 4; i += 2 * WAVE) o[4 + i] = be_byte(wd, i);

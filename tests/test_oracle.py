@@ -190,3 +190,27 @@ def test_kbd_window_matches_window_py():
     assert np.max(np.abs(w - ref)) < 4e-15
     assert np.max(np.abs(w[:1024] ** 2 + w[1024:] ** 2 - 1.0)) < 5e-16
     assert np.array_equal(P.Oracle(48000).window(), np.sin((np.arange(2048) + 0.5) * np.pi / 2048))
+
+
+def test_mono_master_first_block_is_stereo_left():
+    """Mono master extension (parity unpinned: not in the reference).  Tie
+    to the pinned stereo coder: with R silent every band codes L/R (LRMS 0),
+    and before the reservoir diverges (block 0: nothing withdrawn yet) the
+    mono channel-block equals the stereo stream's left channel-block; the
+    decode reconstructs the signal."""
+    import struct
+    from pac_amd import synth
+    fs = 48000
+    x = synth.pink_tones_pcm(6 * 1024 + 5, fs, seed=3)
+    mono = np.ascontiguousarray(x[:, :1])
+    st = np.zeros_like(x)
+    st[:, 0] = x[:, 0]
+    o = P.Oracle(fs, huffman=True)
+    m = o.encode_data(P.MASTER, mono)
+    s = o.encode_data(P.MASTER, st)
+    n0 = struct.unpack("<L", m[:4])[0]
+    assert m[:4 + n0] == s[:4 + n0]
+    d = o.decode_data(P.MASTER, m, 1)
+    a = mono[:, 0].astype(float)
+    b = d[:len(a), 0].astype(float)
+    assert 10 * np.log10((a ** 2).sum() / ((a - b) ** 2).sum()) > 10.0

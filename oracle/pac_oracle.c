@@ -36,6 +36,8 @@
 #define N 2048
 #define HALFN 1024
 #define NB 25
+#define NS 512              /* block-switching extension: short block */
+#define HALFS 256
 
 /* ------------------------------------------------------------------------ */
 /* tables                                                                   */
@@ -70,6 +72,14 @@ struct pac_oracle {
     /* IMDCT twiddles, mdct.py:75,79 */
     double ipre_c[N], ipre_s[N];    /* exp(j 2 pi k n0 / N) */
     double ipost_c[N], ipost_s[N];  /* exp(j 2 pi (n + n0) / 2N) */
+    /* block-switching extension (not in the reference, parity unpinned): the
+     * short transform N = 512 (256 lines), its window, and the masking model's
+     * tables at N = 512 (the same psychoac.py formulas with N = 512) */
+    int bs;
+    double sine_s[NS], hann_s[NS];
+    double cos_s[2048];             /* cos(pi p / 1024): MDCT/IMDCT N=512 kernels */
+    double dft_c[NS], dft_s[NS];    /* exp(-j 2 pi p / 512) */
+    double bark_line_s[HALFS], tiq_s[HALFS], bark_bin_s[HALFS], mld_s[HALFS];
 };
 
 static double Bark(double f) {       /* psychoac.py:56-64 */
@@ -135,25 +145,34 @@ static long double bessel_i0l(long double x) {
     return sum;
 }
 
-void pac_oracle_set_window(pac_oracle *t, int kind) {
-    if (kind == 1) {
-        long double k2[N / 2 + 1], den = 0.0L, cum = 0.0L;
-        const long double pa = (long double)M_PI * 4.0L, norm = bessel_i0l(pa);
-        for (int i = 0; i <= N / 2; i++) {
-            const long double r = 4.0L * i / N - 1.0L;
-            const long double kv = bessel_i0l(pa * sqrtl(fmaxl(0.0L, 1.0L - r * r))) / norm;
-            k2[i] = kv * kv;
-            den += k2[i];
-        }
-        for (int i = 0; i < N / 2; i++) {
-            cum += k2[i];
-            t->sine[i] = (double)sqrtl(cum / den);
-            t->sine[N - 1 - i] = t->sine[i];
-        }
-    } else {
-        for (int n = 0; n < N; n++) t->sine[n] = sin(((double)n + 0.5) * M_PI / (double)N);
+static void kbd_window(int n, double *w) {
+    long double k2[N / 2 + 1], den = 0.0L, cum = 0.0L;
+    const long double pa = (long double)M_PI * 4.0L, norm = bessel_i0l(pa);
+    for (int i = 0; i <= n / 2; i++) {
+        const long double r = 4.0L * i / n - 1.0L;
+        const long double kv = bessel_i0l(pa * sqrtl(fmaxl(0.0L, 1.0L - r * r))) / norm;
+        k2[i] = kv * kv;
+        den += k2[i];
+    }
+    for (int i = 0; i < n / 2; i++) {
+        cum += k2[i];
+        w[i] = (double)sqrtl(cum / den);
+        w[n - 1 - i] = w[i];
     }
 }
+
+/* the MDCT windows, long (N = 2048) and, for block switching, short (512) */
+void pac_oracle_set_window(pac_oracle *t, int kind) {
+    if (kind == 1) {
+        kbd_window(N, t->sine);
+        kbd_window(NS, t->sine_s);
+    } else {
+        for (int n = 0; n < N; n++) t->sine[n] = sin(((double)n + 0.5) * M_PI / (double)N);
+        for (int n = 0; n < NS; n++) t->sine_s[n] = sin(((double)n + 0.5) * M_PI / (double)NS);
+    }
+}
+
+void pac_oracle_set_block_switch(pac_oracle *t, int on) { t->bs = on ? 1 : 0; }
 
 double pac_oracle_window(const pac_oracle *t, int n) { return t->sine[n]; }
 
@@ -224,6 +243,30 @@ pac_oracle *pac_oracle_create(int fs) {
             if (v > mx) mx = v;
         }
         for (int k = 0; k < HALFN; k++) t->mld[k] = t->mld[k] / mx;
+    }
+    /* block-switching extension tables (N = 512, 256 lines) */
+    for (int n = 0; n < NS; n++) {
+        t->sine_s[n] = sin(((double)n + 0.5) * M_PI / (double)NS);
+        t->hann_s[n] = 0.5 * (1 - cos(2.0 * ((double)n + 0.5) * M_PI / (double)NS));
+        t->dft_c[n] = cos(-2.0 * M_PI * (double)n / (double)NS);
+        t->dft_s[n] = sin(-2.0 * M_PI * (double)n / (double)NS);
+    }
+    for (int p = 0; p < 2048; p++) t->cos_s[p] = cos(M_PI * (double)p / 1024.0);
+    {
+        const int step_s = fs / NS;
+        double mx = -1.0;
+        for (int k = 0; k < HALFS; k++) {
+            double f = fs / 2.0 / (double)HALFS * ((double)k + 0.5);
+            t->bark_line_s[k] = Bark(f);
+            t->tiq_s[k] = Intensity(Thresh(f));
+            t->bark_bin_s[k] = Bark((double)(k * step_s));
+            double f2 = (((double)k + 0.5) / (double)HALFS) * (fs / 2.0);
+            double fm = f2 < 3000. ? f2 : 3000.;
+            double v = pow(10.0, 1.25 * (1 - cos(M_PI * (fm / 3000.))) - 2.5);
+            t->mld_s[k] = v;
+            if (v > mx) mx = v;
+        }
+        for (int k = 0; k < HALFS; k++) t->mld_s[k] = t->mld_s[k] / mx;
     }
     return t;
 }
@@ -546,9 +589,9 @@ static void quantize_bands(const pac_oracle *t, const double *lines, const int *
     }
 }
 
-static void mdct_and_scale(const pac_oracle *t, double *x, double *X, int *overall,
-                           double *X_unscaled) {
-    for (int n = 0; n < N; n++) x[n] *= t->sine[n];          /* SineWindow in place */
+static void mdct_and_scale_w(const pac_oracle *t, double *x, double *X, const double *win, int *overall,
+                             double *X_unscaled) {
+    for (int n = 0; n < N; n++) x[n] *= win[n];              /* SineWindow in place */
     pac_oracle_mdct(t, x, X);
     if (X_unscaled) memcpy(X_unscaled, X, sizeof(double) * HALFN);
     double mx = 0.0;
@@ -556,6 +599,150 @@ static void mdct_and_scale(const pac_oracle *t, double *x, double *X, int *overa
     *overall = scale_factor(mx, 4, 5);
     double g = (double)(1 << *overall);
     for (int k = 0; k < HALFN; k++) X[k] *= g;
+}
+
+static void mdct_and_scale(const pac_oracle *t, double *x, double *X, int *overall, double *X_unscaled) {
+    mdct_and_scale_w(t, x, X, t->sine, overall, X_unscaled);
+}
+
+/* ------------------------------------------------------------------------ */
+/* block switching: an EXTENSION, not in the reference (pacfile.py:23,48 has */
+/* no block switching), so parity is unpinned.  Design:        */
+/*  - every frame still takes one 1024-sample hop; a frame is LONG (one     */
+/*    N = 2048 MDCT, mdct.py with a = b = 1024) or SHORT (four N = 512 MDCTs */
+/*    at buffer offsets 384 + 256 k, mdct.py with a = b = 256), the short   */
+/*    spectra interleaved line 4 j + k so the 25-band layout, bit           */
+/*    allocation, quantizer, Huffman and bitstream are the long ones;       */
+/*  - a long frame next to a short one takes the short window's slope over  */
+/*    the short blocks' overlap and 0 / 1 outside it (start / stop shapes); */
+/*  - attack in a frame's new half: first-difference energy of a 128-sample */
+/*    segment > 10 x the mean of the 8 before it and > 1e-3; a frame is     */
+/*    short when it or the frame before has an attack;                      */
+/*  - the masking model of a short block is psychoac.py's calcBTHR at       */
+/*    N = 512 (same formulas), per short block, interleaved like the lines; */
+/*  - one bit after the LRMS bits marks a short frame.                      */
+/* ------------------------------------------------------------------------ */
+
+/* attack in the new half of one channel's 2048-sample block */
+static int bs_attack(const double *x) {
+    double E[16];
+    for (int sg = 0; sg < 16; sg++) {
+        double e = 0.0;
+        for (int n = 128 * sg; n < 128 * sg + 128; n++) {
+            const double d = n ? x[n] - x[n - 1] : 0.0;
+            e += d * d;
+        }
+        E[sg] = e;
+    }
+    for (int sg = 8; sg < 16; sg++) {
+        double m = 0.0;
+        for (int j = sg - 8; j < sg; j++) m += E[j];
+        if (E[sg] > PAC_BS_RATIO * (m / 8.0) && E[sg] > PAC_BS_EMIN) return 1;
+    }
+    return 0;
+}
+
+/* MDCT window of a long frame: the long window, with the short window's
+ * slope (and 0 / 1) on a side whose neighbour frame is short */
+static void bs_long_window(const pac_oracle *t, int fl, double *w) {
+    memcpy(w, t->sine, sizeof(double) * N);
+    if (fl & PAC_BS_PREV)
+        for (int n = 0; n < HALFN; n++) w[n] = n < 384 ? 0.0 : (n < 640 ? t->sine_s[n - 384] : 1.0);
+    if (fl & PAC_BS_NEXT)
+        for (int n = HALFN; n < N; n++) w[n] = n < 1408 ? 1.0 : (n < 1664 ? t->sine_s[n - 1408 + 256] : 0.0);
+}
+
+/* MDCT (mdct.py:49-82, a = b = 256, n0 = 128.5) by its defining sum; an
+ * exactly-zero line is +0.0 */
+static void mdct512(const pac_oracle *t, const double *x, double *X) {
+    for (int j = 0; j < HALFS; j++) {
+        double acc = 0.0;
+        for (int i = 0; i < NS; i++) acc += x[i] * t->cos_s[((2 * i + 257) * (2 * j + 1)) & 2047];
+        acc = (2. / NS) * acc;
+        X[j] = acc == 0.0 ? 0.0 : acc;
+    }
+}
+
+/* IMDCT (mdct.py:72-79, a = b = 256): 2 sum_j X[j] cos(2 pi/N (i + n0)(j + 1/2)) */
+static void imdct512(const pac_oracle *t, const double *X, double *y) {
+    for (int i = 0; i < NS; i++) {
+        double acc = 0.0;
+        for (int j = 0; j < HALFS; j++) acc += X[j] * t->cos_s[((2 * i + 257) * (2 * j + 1)) & 2047];
+        y[i] = 2.0 * acc;
+    }
+}
+
+/* the four short MDCTs of a short frame, interleaved (line 4 j + k), and the
+ * overall scale; seg[k] = the windowed short block k (the in-place chain the
+ * thresholds continue, as mdct_and_scale leaves x) */
+static void short_mdct_and_scale(const pac_oracle *t, const double *x, double *X, double seg[4][NS],
+                                 int *overall, double *X_unscaled) {
+    double Xk[HALFS];
+    for (int k = 0; k < 4; k++) {
+        for (int i = 0; i < NS; i++) seg[k][i] = x[384 + 256 * k + i] * t->sine_s[i];
+        mdct512(t, seg[k], Xk);
+        for (int j = 0; j < HALFS; j++) X[4 * j + k] = Xk[j];
+    }
+    if (X_unscaled) memcpy(X_unscaled, X, sizeof(double) * HALFN);
+    double mx = 0.0;
+    for (int k = 0; k < HALFN; k++) { double a = fabs(X[k]); if (a > mx) mx = a; }
+    *overall = scale_factor(mx, 4, 5);
+    double g = (double)(1 << *overall);
+    for (int k = 0; k < HALFN; k++) X[k] *= g;
+}
+
+/* calcBTHR (psychoac.py:409-456) of a short block, N = 512, by the same
+ * formulas as pac_oracle_threshold; Hann in place first */
+static int threshold_short(const pac_oracle *t, double *data, int noDrop, double *thr) {
+    double mag[HALFS], I[HALFS];
+    for (int n = 0; n < NS; n++) data[n] *= t->hann_s[n];
+    for (int k = 0; k < HALFS; k++) {
+        double re = 0.0, im = 0.0;
+        for (int n = 0; n < NS; n++) {
+            const int p = (n * k) & (NS - 1);
+            re += data[n] * t->dft_c[p];
+            im += data[n] * t->dft_s[p];
+        }
+        mag[k] = hypot(re, im);
+        I[k] = 0.0;
+    }
+    const double drop = noDrop ? 0.0 : 15.0;
+    const double csp = 8.0 / 3.0 * 4.0 / ((double)NS * (double)NS);
+    int np = 0;
+    for (int k = 1; k < HALFS - 1; k++) {
+        double m = mag[k];
+        if (!(m > mag[k - 1] && m > mag[k + 1] && 10.0 * log10(m) > -30.0)) continue;
+        np++;
+        double s = 0.0;
+        if (k - 3 >= 0) {
+            int hi = k + 3 < HALFS ? k + 3 : HALFS;
+            for (int j = k - 3; j < hi; j++) s += mag[j] * mag[j];
+        }
+        double S = SPL(csp * s);
+        double zm = t->bark_bin_s[k];
+        double lev = S - 40.0;
+        lev = 0.367 * (0 > lev ? 0.0 : lev);
+        for (int l = 0; l < HALFS; l++) {
+            double dz = t->bark_line_s[l] - zm;
+            double A = (dz >= 0 ? lev : 0.0) - 27.0;
+            double ad = fabs(dz);
+            double B = ad > 0.5 ? (ad - 0.5) : 0.0;
+            double spl = S + A * B - drop;
+            I[l] += pow(10.0, (spl - 96.0) / 10.0);
+        }
+    }
+    for (int l = 0; l < HALFS; l++) thr[l] = SPL(I[l] + t->tiq_s[l]);
+    return np;
+}
+
+/* block-switching flags of every block of a stream from the attack flags */
+static void bs_flags(const uint8_t *att, int64_t nblocks, uint8_t *fl) {
+    for (int64_t b = 0; b < nblocks; b++) {
+        const int sh = att[b] || (b > 0 && att[b - 1]);
+        const int pv = b > 0 && (att[b - 1] || (b > 1 && att[b - 2]));
+        const int nx = b + 1 < nblocks && (att[b + 1] || att[b]);
+        fl[b] = (uint8_t)((sh ? PAC_BS_SHORT : 0) | (pv ? PAC_BS_PREV : 0) | (nx ? PAC_BS_NEXT : 0));
+    }
 }
 
 /* Origin EncodeSingleChannel (PerceptualAudioCodec_Origin/codec/codec.py:70-151)
@@ -631,9 +818,10 @@ static long withdraw(long *deposit) {
  * modified in place like the reference.  xR == NULL: the mono master
  * extension (not in the reference, parity unpinned) -- LRMS all 0, channel 0
  * alone: BTHR_L, its SMRs, one BitAlloc + Huffman + deposit per block. */
-void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
-                             pac_oracle_state *st, pac_oracle_stblock *o) {
+static void block_master_core(const pac_oracle *t, double *xL, double *xR, int fl,
+                              pac_oracle_state *st, pac_oracle_stblock *o) {
     const int nch = xR ? 2 : 1;
+    const int sh = fl & PAC_BS_SHORT;
     memset(o->lrms, 0, sizeof(o->lrms));
     /* LRMS decision on the raw (unwindowed) blocks codec.py:94-102 */
     if (nch == 2) {
@@ -668,9 +856,18 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
     o->extra_in = st->extraBits;
 
     double XL[HALFN], XR[HALFN];
-    mdct_and_scale(t, xL, XL, &o->overall[0], o->mdct[0]);
+    double segL[4][NS], segR[4][NS];           /* short frames: the windowed short blocks */
+    double wl[N];
+    const double *win = t->sine;
+    if (fl & (PAC_BS_PREV | PAC_BS_NEXT)) {
+        bs_long_window(t, fl, wl);
+        win = wl;
+    }
+    if (sh) short_mdct_and_scale(t, xL, XL, segL, &o->overall[0], o->mdct[0]);
+    else mdct_and_scale_w(t, xL, XL, win, &o->overall[0], o->mdct[0]);
     if (nch == 2) {
-        mdct_and_scale(t, xR, XR, &o->overall[1], o->mdct[1]);
+        if (sh) short_mdct_and_scale(t, xR, XR, segR, &o->overall[1], o->mdct[1]);
+        else mdct_and_scale_w(t, xR, XR, win, &o->overall[1], o->mdct[1]);
     } else {
         memset(XR, 0, sizeof(XR));
         o->overall[1] = 0;
@@ -688,8 +885,28 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
         splM[k] = SPL(4. * (M[k] * M[k])) - gL;
         splS[k] = SPL(4. * (S[k] * S[k])) - gR;
     }
+    if (sh) {            /* short frame: calcBTHR per short block at N = 512, interleaved */
+        for (int v = 0; v < 6; v++) o->npeaks[v] = 0;
+        for (int k = 0; k < 4; k++) {
+            double th[HALFS], dM[NS], dS[NS];
+            const int nv = nch == 2 ? 6 : 1;
+            for (int v = 0; v < nv; v++) {
+                if (v == 2)
+                    for (int n = 0; n < NS; n++) {
+                        dM[n] = (segL[k][n] + segR[k][n]) / 2.0;
+                        dS[n] = (segL[k][n] - segR[k][n]) / 2.0;
+                    }
+                double *d = v == 0 ? segL[k] : v == 1 ? segR[k] : (v & 1) ? dS : dM;
+                o->npeaks[v] += threshold_short(t, d, v >= 4, th);
+                for (int j = 0; j < HALFS; j++) o->bthr[v][4 * j + k] = th[j];
+            }
+        }
+        if (nch == 1) goto smr_mono;
+        goto combine;
+    }
     o->npeaks[0] = pac_oracle_threshold(t, xL, 0, o->bthr[0], NULL);   /* BTHR_L */
     if (nch == 1) {
+    smr_mono:
         for (int b = 0; b < NB; b++) {
             double lr0 = -INFINITY;
             for (int l = t->lower[b]; l <= t->upper[b]; l++) {
@@ -711,10 +928,12 @@ void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
     o->npeaks[3] = pac_oracle_threshold(t, dS, 0, o->bthr[3], NULL);   /* BTHR_S */
     o->npeaks[4] = pac_oracle_threshold(t, dM, 1, o->bthr[4], NULL);   /* BTHR_M_MLD */
     o->npeaks[5] = pac_oracle_threshold(t, dS, 1, o->bthr[5], NULL);   /* BTHR_S_MLD */
+combine:;
     double thrM[HALFN], thrS[HALFN];
     for (int k = 0; k < HALFN; k++) {
-        double mldM = o->bthr[4][k] * t->mld[k];
-        double mldS = o->bthr[5][k] * t->mld[k];
+        const double mld = sh ? t->mld_s[k >> 2] : t->mld[k];
+        double mldM = o->bthr[4][k] * mld;
+        double mldS = o->bthr[5][k] * mld;
         double a = o->bthr[3][k] < mldS ? o->bthr[3][k] : mldS;
         thrM[k] = o->bthr[2][k] > a ? o->bthr[2][k] : a;
         double c = o->bthr[2][k] < mldM ? o->bthr[2][k] : mldM;
@@ -759,6 +978,11 @@ alloc:
     o->deposit_out = st->deposit;
 }
 
+void pac_oracle_block_master(const pac_oracle *t, double *xL, double *xR,
+                             pac_oracle_state *st, pac_oracle_stblock *o) {
+    block_master_core(t, xL, xR, 0, st, o);
+}
+
 /* ------------------------------------------------------------------------ */
 /* bitstream (pacfile.py:288-351, bitpack.py:36-101)                        */
 /* ------------------------------------------------------------------------ */
@@ -792,9 +1016,10 @@ static int64_t emit_origin(const pac_oracle *t, const pac_oracle_chblock *o, uin
     return k + nbytes;
 }
 
+/* bsbit >= 0: block switching on, the frame's short flag after the LRMS bits */
 static int64_t emit_master(const pac_oracle *t, const pac_oracle_stblock *o, int ch,
-                           uint8_t *out) {
-    int nbytes = (o->nbits[ch] + 7) / 8;
+                           uint8_t *out, int bsbit) {
+    int nbytes = (o->nbits[ch] + (bsbit >= 0) + 7) / 8;
     int64_t k = write_u32le(out, (uint32_t)nbytes);
     memset(out + k, 0, nbytes);
     bw w = {out + k, 0};
@@ -818,6 +1043,7 @@ static int64_t emit_master(const pac_oracle *t, const pac_oracle_stblock *o, int
         }
     }
     for (int b = 0; b < NB; b++) put(&w, (uint32_t)o->lrms[b], 1);
+    if (bsbit >= 0) put(&w, (uint32_t)bsbit, 1);
     return k + nbytes;
 }
 
@@ -870,7 +1096,11 @@ static double dequantize(int scale, int64_t m, int ba) {
 }
 
 /* IMDCT mdct.py:72-79 (a=b=1024, numpy formula) followed by SineWindow */
+static void imdct_window_w(const pac_oracle *t, const double *X, double *y, const double *win);
 void pac_oracle_imdct_window(const pac_oracle *t, const double *X, double *y) {
+    imdct_window_w(t, X, y, t->sine);
+}
+static void imdct_window_w(const pac_oracle *t, const double *X, double *y, const double *win) {
     double re[N], im[N];
     for (int k = 0; k < N; k++) {
         const double v = k < HALFN ? X[k] : -X[N - 1 - k];     /* hstack((data, -data[::-1])) */
@@ -881,7 +1111,7 @@ void pac_oracle_imdct_window(const pac_oracle *t, const double *X, double *y) {
     for (int n = 0; n < N; n++) {
         const double ar = re[n] / (double)N, ai = -im[n] / (double)N;   /* numpy ifft: 1/N */
         const double post = (double)N * (ar * t->ipost_c[n] - ai * t->ipost_s[n]);
-        y[n] = post * t->sine[n];
+        y[n] = post * win[n];
     }
 }
 
@@ -896,7 +1126,7 @@ int16_t pac_oracle_float_to_pcm(double x) {
 
 /* one channel-block's fields from its nBytes of data */
 static void parse_chblock(const pac_oracle *t, int profile, const uint8_t *p, int64_t n, int *overall,
-                          int *ba, int *sf, int64_t *mant, int *lrms) {
+                          int *ba, int *sf, int64_t *mant, int *lrms, int *bsbit) {
     br r = {p, n, 0};
     *overall = (int)get(&r, 4);
     int id = profile == PAC_ORACLE_MASTER ? (int)get(&r, 4) - 1 : 0;
@@ -918,6 +1148,7 @@ static void parse_chblock(const pac_oracle *t, int profile, const uint8_t *p, in
     }
     if (profile == PAC_ORACLE_MASTER)
         for (int b = 0; b < NB; b++) lrms[b] = (int)get(&r, 1);
+    if (bsbit) *bsbit = (int)get(&r, 1);     /* block-switching extension: short frame */
 }
 
 /* Decode the data section of a .pac/.wak file (everything after the header)
@@ -929,72 +1160,98 @@ int64_t pac_oracle_decode(const pac_oracle *t, int profile, const uint8_t *data,
                           int16_t *pcm, double *fout, int64_t max_frames) {
     if (n_ch < 1 || n_ch > 8) return -1;
     if (profile == PAC_ORACLE_MASTER && (n_ch > 2 || !t->have_huff)) return -1;
+    if (t->bs && profile != PAC_ORACLE_MASTER) return -1;
+    /* pass 1: every block's dequantized lines (and block-switching flag) */
+    int64_t nfr = 0, cap = 16;
+    double *lines = (double *)malloc((size_t)cap * n_ch * HALFN * sizeof(double));
+    uint8_t *sh = (uint8_t *)malloc((size_t)cap);
+    int64_t *mant = (int64_t *)malloc((size_t)HALFN * sizeof(int64_t));
     double *prev = (double *)calloc((size_t)n_ch * HALFN, sizeof(double));
-    double *lines = (double *)malloc((size_t)n_ch * HALFN * sizeof(double));
     double *y = (double *)malloc((size_t)n_ch * N * sizeof(double));
-    int64_t *mant = (int64_t *)malloc((size_t)n_ch * HALFN * sizeof(int64_t));
     int64_t pos = 0, frames = 0;
-    int first = 1, ret = 0;
-    for (;;) {
-        int eof = pos + 4 > nbytes;
-        int lrms[NB] = {0};
-        if (!eof) {
-            for (int c = 0; c < n_ch; c++) {
-                if (pos + 4 > nbytes) { ret = -3; goto done; }
-                uint32_t nb = (uint32_t)data[pos] | ((uint32_t)data[pos + 1] << 8) |
-                              ((uint32_t)data[pos + 2] << 16) | ((uint32_t)data[pos + 3] << 24);
-                pos += 4;
-                if (pos + (int64_t)nb > nbytes) { ret = -3; goto done; }
-                int overall, ba[NB], sf[NB];
-                parse_chblock(t, profile, data + pos, nb, &overall, ba, sf, mant + c * HALFN, lrms);
-                pos += nb;
-                /* codec.Decode: dequantize the bands with bits, then / 2^overall */
-                double *L = lines + c * HALFN;
-                memset(L, 0, sizeof(double) * HALFN);
-                for (int b = 0; b < NB; b++)
-                    if (ba[b])
-                        for (int l = t->lower[b]; l <= t->upper[b]; l++)
-                            L[l] = dequantize(sf[b], mant[c * HALFN + l], ba[b]);
-                const double rescale = 1. * (double)(1 << overall);
-                for (int l = 0; l < HALFN; l++) L[l] /= rescale;
-            }
-            if (profile == PAC_ORACLE_MASTER && n_ch == 2) {
-                /* codec.py:46-54.  mdctLineL/R ALIAS mdctLine[0]/[1], so the
-                 * second assignment reads the already-updated channel 0:
-                 * L = M - S, R = (M - S) + S */
-                double *A = lines, *B = lines + HALFN;
-                for (int b = 0; b < NB; b++) {
-                    if (!lrms[b]) continue;
-                    for (int l = t->lower[b]; l <= t->upper[b]; l++) {
-                        A[l] = A[l] - B[l];
-                        B[l] = A[l] + B[l];
-                    }
+    int ret = 0;
+    while (pos + 4 <= nbytes) {
+        if (nfr == cap) {
+            cap *= 2;
+            lines = (double *)realloc(lines, (size_t)cap * n_ch * HALFN * sizeof(double));
+            sh = (uint8_t *)realloc(sh, (size_t)cap);
+        }
+        int lrms[NB] = {0}, bsb = 0;
+        for (int c = 0; c < n_ch; c++) {
+            if (pos + 4 > nbytes) { ret = -3; goto done; }
+            uint32_t nb = (uint32_t)data[pos] | ((uint32_t)data[pos + 1] << 8) |
+                          ((uint32_t)data[pos + 2] << 16) | ((uint32_t)data[pos + 3] << 24);
+            pos += 4;
+            if (pos + (int64_t)nb > nbytes) { ret = -3; goto done; }
+            int overall, ba[NB], sf[NB];
+            parse_chblock(t, profile, data + pos, nb, &overall, ba, sf, mant, lrms, t->bs ? &bsb : NULL);
+            pos += nb;
+            /* codec.Decode: dequantize the bands with bits, then / 2^overall */
+            double *L = lines + (nfr * n_ch + c) * HALFN;
+            memset(L, 0, sizeof(double) * HALFN);
+            for (int b = 0; b < NB; b++)
+                if (ba[b])
+                    for (int l = t->lower[b]; l <= t->upper[b]; l++) L[l] = dequantize(sf[b], mant[l], ba[b]);
+            const double rescale = 1. * (double)(1 << overall);
+            for (int l = 0; l < HALFN; l++) L[l] /= rescale;
+        }
+        if (profile == PAC_ORACLE_MASTER && n_ch == 2) {
+            /* codec.py:46-54.  mdctLineL/R ALIAS mdctLine[0]/[1], so the
+             * second assignment reads the already-updated channel 0:
+             * L = M - S, R = (M - S) + S */
+            double *A = lines + nfr * 2 * HALFN, *B = A + HALFN;
+            for (int b = 0; b < NB; b++) {
+                if (!lrms[b]) continue;
+                for (int l = t->lower[b]; l <= t->upper[b]; l++) {
+                    A[l] = A[l] - B[l];
+                    B[l] = A[l] + B[l];
                 }
             }
-            for (int c = 0; c < n_ch; c++) pac_oracle_imdct_window(t, lines + c * HALFN, y + c * N);
         }
-        if (!eof || 1) {
-            /* ReadDataBlock's result: overlap-add of the first half (or, at
-             * the end of the file, the saved half alone) */
-            if (!first) {
-                if (frames + HALFN > max_frames) { ret = -2; goto done; }
-                for (int i = 0; i < HALFN; i++)
-                    for (int c = 0; c < n_ch; c++) {
-                        double v = eof ? prev[c * HALFN + i] : prev[c * HALFN + i] + y[c * N + i];
-                        int64_t o = (frames + i) * n_ch + c;
-                        pcm[o] = pac_oracle_float_to_pcm(v);
-                        if (fout) fout[o] = v;
+        sh[nfr++] = (uint8_t)bsb;
+    }
+    /* pass 2: synthesis and the driver's output (ReadDataBlock results: the
+     * first one skipped, the saved half alone at the end of the file) */
+    for (int64_t f = 0; f <= nfr; f++) {
+        const int eof = f == nfr;
+        if (!eof) {
+            for (int c = 0; c < n_ch; c++) {
+                const double *X = lines + (f * n_ch + c) * HALFN;
+                double *yc = y + c * N;
+                if (sh[f]) {        /* block switching: four short blocks, windowed, overlap-added */
+                    double Xk[HALFS], u[NS];
+                    memset(yc, 0, sizeof(double) * N);
+                    for (int k = 0; k < 4; k++) {
+                        for (int j = 0; j < HALFS; j++) Xk[j] = X[4 * j + k];
+                        imdct512(t, Xk, u);
+                        for (int i = 0; i < NS; i++) yc[384 + 256 * k + i] += u[i] * t->sine_s[i];
                     }
-                frames += HALFN;
+                } else {
+                    const int fl = (f > 0 && sh[f - 1] ? PAC_BS_PREV : 0) | (f + 1 < nfr && sh[f + 1] ? PAC_BS_NEXT : 0);
+                    double wl[N];
+                    const double *win = t->sine;
+                    if (fl) { bs_long_window(t, fl, wl); win = wl; }
+                    imdct_window_w(t, X, yc, win);
+                }
             }
-            first = 0;
+        }
+        if (f > 0) {
+            if (frames + HALFN > max_frames) { ret = -2; goto done; }
+            for (int i = 0; i < HALFN; i++)
+                for (int c = 0; c < n_ch; c++) {
+                    double v = eof ? prev[c * HALFN + i] : prev[c * HALFN + i] + y[c * N + i];
+                    int64_t o = (frames + i) * n_ch + c;
+                    pcm[o] = pac_oracle_float_to_pcm(v);
+                    if (fout) fout[o] = v;
+                }
+            frames += HALFN;
         }
         if (eof) break;
         for (int c = 0; c < n_ch; c++) memcpy(prev + c * HALFN, y + c * N + HALFN, sizeof(double) * HALFN);
     }
     ret = 0;
 done:
-    free(prev); free(lines); free(y); free(mant);
+    free(prev); free(lines); free(y); free(mant); free(sh);
     return ret < 0 ? ret : frames;
 }
 
@@ -1002,13 +1259,88 @@ done:
 /* whole stream: PACFile.WriteDataBlock loop + Close flush                  */
 /* ------------------------------------------------------------------------ */
 
+/* block blk of a stream as PACFile.WriteDataBlock sees it: priorBlock ++ the
+ * hop (zeros past the data and for the Close() flush block), channel c */
+static void fill_block(const int16_t *pcm, int64_t n_frames, int n_ch, int64_t hops, int64_t blk, int c,
+                       double *x) {
+    for (int h = 0; h < 2; h++) {
+        const int64_t b = blk - 1 + h;
+        for (int i = 0; i < HALFN; i++) {
+            const int64_t fr = b * HALFN + i;
+            x[h * HALFN + i] = (b >= 0 && b < hops && fr < n_frames) ? pac_oracle_pcm_to_float(pcm[fr * n_ch + c])
+                                                                      : 0.0;
+        }
+    }
+}
+
+int64_t pac_oracle_bs_plan(const pac_oracle *t, const int16_t *pcm, int64_t n_frames, int n_ch,
+                           uint8_t *flags, int64_t cap) {
+    (void)t;
+    const int64_t hops = (n_frames + HALFN - 1) / HALFN, nblocks = hops + 1;
+    if (cap < nblocks) return -1;
+    uint8_t *att = (uint8_t *)calloc((size_t)nblocks, 1);
+    double x[N];
+    for (int64_t b = 0; b < nblocks; b++)
+        for (int c = 0; c < n_ch; c++) {
+            fill_block(pcm, n_frames, n_ch, hops, b, c, x);
+            att[b] |= (uint8_t)bs_attack(x);
+        }
+    bs_flags(att, nblocks, flags);
+    free(att);
+    return nblocks;
+}
+
+/* block-switching design check (no quantization): MDCT analysis + IMDCT
+ * synthesis of every block of a float stream x[n_frames] (one channel) with
+ * the given flags, overlap-added as the decoder does; out[n_frames] */
+void pac_oracle_bs_roundtrip(const pac_oracle *t, const double *x, int64_t n_frames, const uint8_t *fl,
+                             double *out) {
+    const int64_t hops = (n_frames + HALFN - 1) / HALFN;
+    double buf[N], X[HALFN], y[N], prev[HALFN], wl[N], seg[4][NS];
+    memset(prev, 0, sizeof(prev));
+    for (int64_t b = 0; b <= hops; b++) {
+        for (int i = 0; i < N; i++) {
+            const int64_t fr = (b - 1) * HALFN + i;
+            buf[i] = fr >= 0 && fr < n_frames ? x[fr] : 0.0;
+        }
+        int ov;
+        if (fl[b] & PAC_BS_SHORT) {
+            double Xk[HALFS], u[NS];
+            short_mdct_and_scale(t, buf, X, seg, &ov, NULL);
+            for (int k = 0; k < HALFN; k++) X[k] /= (double)(1 << ov);
+            memset(y, 0, sizeof(y));
+            for (int k = 0; k < 4; k++) {
+                for (int j = 0; j < HALFS; j++) Xk[j] = X[4 * j + k];
+                imdct512(t, Xk, u);
+                for (int i = 0; i < NS; i++) y[384 + 256 * k + i] += u[i] * t->sine_s[i];
+            }
+        } else {
+            bs_long_window(t, fl[b], wl);
+            for (int i = 0; i < N; i++) buf[i] *= wl[i];
+            pac_oracle_mdct(t, buf, X);
+            imdct_window_w(t, X, y, wl);
+        }
+        for (int i = 0; i < HALFN; i++) {
+            const int64_t fr = (b - 1) * HALFN + i;
+            if (fr >= 0 && fr < n_frames) out[fr] = prev[i] + y[i];
+            prev[i] = y[HALFN + i];
+        }
+    }
+}
+
 int64_t pac_oracle_encode(const pac_oracle *t, int profile, const int16_t *pcm,
                           int64_t n_frames, int n_ch, int64_t max_blocks,
                           uint8_t *out, int64_t cap, pac_oracle_state *state) {
     if (profile == PAC_ORACLE_MASTER && (n_ch > 2 || !t->have_huff)) return -1;   /* 1: mono extension */
     if (n_ch < 1 || n_ch > 8) return -1;
+    if (t->bs && profile != PAC_ORACLE_MASTER) return -1;
     int64_t hops = (n_frames + HALFN - 1) / HALFN;
     int64_t nblocks = hops + 1;                     /* + Close() flush block */
+    uint8_t *fl = NULL;
+    if (t->bs) {
+        fl = (uint8_t *)calloc((size_t)nblocks, 1);
+        pac_oracle_bs_plan(t, pcm, n_frames, n_ch, fl, nblocks);
+    }
     if (max_blocks >= 0 && max_blocks < nblocks) nblocks = max_blocks;
     double *prior = (double *)calloc((size_t)n_ch * HALFN, sizeof(double));
     double *full = (double *)malloc((size_t)n_ch * N * sizeof(double));
@@ -1036,12 +1368,13 @@ int64_t pac_oracle_encode(const pac_oracle *t, int profile, const int16_t *pcm,
                 pos += emit_origin(t, co, out + pos);
             }
         } else {
-            pac_oracle_block_master(t, full, n_ch == 2 ? full + N : NULL, st, so);
-            for (int c = 0; c < n_ch; c++) pos += emit_master(t, so, c, out + pos);
+            const int f = fl ? fl[blk] : 0;
+            block_master_core(t, full, n_ch == 2 ? full + N : NULL, f, st, so);
+            for (int c = 0; c < n_ch; c++) pos += emit_master(t, so, c, out + pos, fl ? (f & PAC_BS_SHORT) : -1);
         }
     }
     ret = pos;
 done:
-    free(prior); free(full); free(co); free(so);
+    free(prior); free(full); free(co); free(so); free(fl);
     return ret;
 }

@@ -8,6 +8,12 @@
 #define PAC_ORACLE_MASTER 1
 #define PAC_NTABLES 10
 #define PAC_NSYM 32768
+/* block-switching extension (not in the reference; parity unpinned) */
+#define PAC_BS_SHORT 1      /* four N = 512 blocks, interleaved        */
+#define PAC_BS_PREV 2       /* long frame after a short one (stop)     */
+#define PAC_BS_NEXT 4       /* long frame before a short one (start)   */
+#define PAC_BS_RATIO 10.0
+#define PAC_BS_EMIN 1e-3
 
 typedef struct pac_oracle pac_oracle;
 
@@ -51,6 +57,14 @@ extern "C" {
 pac_oracle *pac_oracle_create(int sample_rate);
 /* MDCT window: 0 SineWindow (the reference coders), 1 KBDWindow alpha 4 (extension) */
 void pac_oracle_set_window(pac_oracle *o, int kind);
+/* block switching on/off (master profile only; extension, parity unpinned) */
+void pac_oracle_set_block_switch(pac_oracle *o, int on);
+/* per-block flags PAC_BS_* the block-switching encoder uses for a stream
+ * (nblocks = hops + 1 flush entries); returns nblocks */
+void pac_oracle_bs_roundtrip(const pac_oracle *o, const double *x, int64_t n_frames, const uint8_t *fl,
+                             double *out);
+int64_t pac_oracle_bs_plan(const pac_oracle *o, const int16_t *pcm, int64_t n_frames, int n_ch,
+                           uint8_t *flags, int64_t cap);
 double pac_oracle_window(const pac_oracle *o, int n);
 void pac_oracle_destroy(pac_oracle *t);
 int pac_oracle_nlines(const pac_oracle *t, int *out25);

@@ -68,6 +68,10 @@ def lib():
         L.pac_oracle_float_to_pcm.restype = C.c_int16
         L.pac_oracle_float_to_pcm.argtypes = [C.c_double]
         L.pac_oracle_set_window.argtypes = [C.c_void_p, C.c_int]
+        L.pac_oracle_set_block_switch.argtypes = [C.c_void_p, C.c_int]
+        L.pac_oracle_bs_plan.restype = C.c_int64
+        L.pac_oracle_bs_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64]
+        L.pac_oracle_bs_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.pac_oracle_window.restype = C.c_double
         L.pac_oracle_window.argtypes = [C.c_void_p, C.c_int]
         L.pac_oracle_encode.restype = C.c_int64
@@ -78,13 +82,15 @@ def lib():
 
 
 class Oracle:
-    def __init__(self, sample_rate, huffman=True, window=0):
+    def __init__(self, sample_rate, huffman=True, window=0, block_switch=False):
         self.L = lib()
         self.h = self.L.pac_oracle_create(int(sample_rate))
         if not self.h:
             raise ValueError("bad sample rate")
         if window:
             self.L.pac_oracle_set_window(self.h, int(window))
+        if block_switch:      # extension, master profile only (parity unpinned)
+            self.L.pac_oracle_set_block_switch(self.h, 1)
         if huffman:
             with open(HUFF, "rb") as f:
                 buf = f.read()
@@ -101,6 +107,24 @@ class Oracle:
 
     def window(self):
         return np.array([self.L.pac_oracle_window(self.h, n) for n in range(2048)])
+
+    def bs_plan(self, pcm):
+        """block-switching flags (PAC_BS_*) of every block of a stream"""
+        pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+        n = (pcm.shape[0] + 1023) // 1024 + 1
+        fl = np.zeros(n, dtype=np.uint8)
+        assert self.L.pac_oracle_bs_plan(self.h, pcm.ctypes.data, pcm.shape[0], pcm.shape[1],
+                                         fl.ctypes.data, n) == n
+        return fl
+
+    def bs_roundtrip(self, x, flags):
+        """unquantized analysis + synthesis of one float channel with these flags"""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        fl = np.ascontiguousarray(flags, dtype=np.uint8)
+        assert fl.shape[0] >= (x.shape[0] + 1023) // 1024 + 1
+        out = np.zeros_like(x)
+        self.L.pac_oracle_bs_roundtrip(self.h, x.ctypes.data, x.shape[0], fl.ctypes.data, out.ctypes.data)
+        return out
 
     def nlines(self):
         out = (C.c_int * 25)()

@@ -51,6 +51,14 @@ typedef struct {
                                        (window.py:56-78) as the MDCT window of
                                        encoder and decoder -- an extension no
                                        reference coder uses (parity unpinned) */
+    int32_t block_switch;           /* 0 (the reference), or 1: block switching
+                                       between one N = 2048 and four N = 512
+                                       MDCTs per frame with attack detection --
+                                       an extension (parity unpinned), master
+                                       profile only, whole streams only (no
+                                       PAC_STREAM_* continuation flags), not
+                                       with pac_encode_block; a short frame is
+                                       marked by one bit after the LRMS bits */
 } pac_params;
 #define PAC_WINDOW_SINE 0
 #define PAC_WINDOW_KBD 1

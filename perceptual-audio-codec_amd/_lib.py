@@ -28,7 +28,7 @@ class Params(C.Structure):
                 ("n_mdct_lines", C.c_int32), ("n_scale_bits", C.c_int32),
                 ("n_mant_size_bits", C.c_int32), ("n_table_id_bits", C.c_int32),
                 ("target_bits_per_sample", C.c_double), ("profile", C.c_int32),
-                ("window", C.c_int32)]
+                ("window", C.c_int32), ("block_switch", C.c_int32)]
 
 
 WINDOW_SINE = 0      # SineWindow (window.py:27-39): the reference coders
@@ -363,7 +363,8 @@ class Context:
         return t
 
 
-def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27, window=WINDOW_SINE):
+def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27, window=WINDOW_SINE,
+           block_switch=False):
     p = Params()
     p.sample_rate = int(sample_rate)
     p.n_channels = int(n_channels)
@@ -374,4 +375,5 @@ def params(sample_rate, n_channels, profile, target_bits_per_sample=2.27, window
     p.target_bits_per_sample = float(target_bits_per_sample)
     p.profile = int(profile)
     p.window = int(window)
+    p.block_switch = 1 if block_switch else 0
     return p

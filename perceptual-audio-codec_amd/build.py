@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "pac_abi.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in
         ("pac_abi.hip", "pac_kernels.hip", "pac_kernels.h", "pac_wave.h", "pac_common.h",
-         "pac_master.hip", "pac_decode.hip", "pac_wav.hip")] + [os.path.join(HERE, "..", "include", "pac_gpu.h")]
+         "pac_master.hip", "pac_decode.hip", "pac_wav.hip", "pac_bs.h")] + [os.path.join(HERE, "..", "include", "pac_gpu.h")]
 LIB = os.path.join(HERE, "libpacgpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -225,6 +225,32 @@ static void build_tables(int fs, int window, PacTables* t) {
             t->pow_mkl[l] = (double)exp2l(-e);
         }
     }
+    {   // block-switching extension tables (pac_bs.h), the same formulas at N = 512
+        for (int n = 0; n < 512; n++) {
+            t->sine_s[n] = sin(((double)n + 0.5) * M_PI / 512.0);
+            t->hann_s[n] = 0.5 * (1 - cos(2.0 * ((double)n + 0.5) * M_PI / 512.0));
+        }
+        if (window == PAC_WINDOW_KBD) kbd_window(512, 4.0, t->sine_s);
+        for (int q = 0; q < 128; q++) {
+            const double a = -M_PI * (q + 0.25) / 256.0, b = -M_PI * q / 256.0;
+            t->mdct_pre_s[q] = make_double2(cos(a), sin(a));
+            t->mdct_post_s[q] = make_double2(cos(b), sin(b));
+        }
+        const int step_s = fs / 512;
+        double mxs = -1.0;
+        for (int k = 0; k < 256; k++) {
+            const double f = fs / 2.0 / 256.0 * ((double)k + 0.5);
+            t->bark_line_s[k] = host_bark(f);
+            t->tiq_s[k] = pow(10.0, (host_thresh(f) - 96.0) / 10.0);
+            t->bark_bin_s[k] = host_bark((double)(k * step_s));
+            const double f2 = (((double)k + 0.5) / 256.0) * (fs / 2.0);
+            const double fm = f2 < 3000. ? f2 : 3000.;
+            const double v = pow(10.0, 1.25 * (1 - cos(M_PI * (fm / 3000.))) - 2.5);
+            t->mld_s[k] = v;
+            if (v > mxs) mxs = v;
+        }
+        for (int k = 0; k < 256; k++) t->mld_s[k] = t->mld_s[k] / mxs;
+    }
     for (int l = 0, ku = 0, kv = 0; l < PAC_HALFN; l++) {   // bark_line ascending in l
         const double zl = t->bark_line[l];
         while (ku < PAC_HALFN - 1 && zl - t->bark_bin[ku] > 0.5) ku++;
@@ -289,6 +315,8 @@ struct pac_ctx {
     DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
     DevBuf<uint64_t> dbg_code;
     DevBuf<uint8_t> dbg_len;
+    DevBuf<uint8_t> bs_att, bs_fl;          // block switching: attack / PAC_BS_* flags per block
+    DevBuf<uint8_t> dec_bsf;                // decoder: the short-frame bit per channel-block
     hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
@@ -522,6 +550,9 @@ static int check_params(const pac_params* p) {
     }
     if (!(p->target_bits_per_sample > 0.0)) return set_err(PAC_E_ARG, "targetBitsPerSample");
     if (p->window != PAC_WINDOW_SINE && p->window != PAC_WINDOW_KBD) return set_err(PAC_E_ARG, "window %d", p->window);
+    if (p->block_switch != 0 && p->block_switch != 1) return set_err(PAC_E_ARG, "block_switch %d", p->block_switch);
+    if (p->block_switch && p->profile != PAC_PROFILE_MASTER)
+        return set_err(PAC_E_UNSUPPORTED, "block switching is built for the master profile");
     return PAC_OK;
 }
 
@@ -726,7 +757,16 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_smr.ensure(2 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(2 * cbmax * 2 * PAC_NB)))
         return rc;
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
-                      nullptr, nullptr, nullptr};
+                      nullptr, nullptr, nullptr, nullptr};
+    if (p->block_switch) {     // pac_bs.h: attack flags, then each block's PAC_BS_* flags
+        if ((rc = c->bs_att.ensure(nblocks + 1)) || (rc = c->bs_fl.ensure(nblocks + 1))) return rc;
+        hipLaunchKernelGGL(k_bs_attack, dim3((unsigned)((nblocks + 1) / 2)), dim3(64), 0, c->stream, src, nblocks,
+                           c->bs_att.p);
+        hipLaunchKernelGGL(k_bs_flags, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, c->stream,
+                           src.blk_off, n_streams, nblocks, c->bs_att.p, c->bs_fl.p);
+        HIPCHK(hipGetLastError());
+        F.bsf = c->bs_fl.p;
+    }
     if (dbg_codes) {
         if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
             (rc = c->dbg_len.ensure(G * PAC_HALFN)))
@@ -767,6 +807,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                 hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
             if ((rc = mark(0, 5))) return rc;
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
+            if (F.bsf)     // the short frames' thresholds (the long kernel skips them)
+                hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(B * nvar)), dim3(256), 0, s0, src, T, K, F,
+                                   ck);
             if ((rc = mark(0, 0))) return rc;
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             HIPCHK(hipGetLastError());
@@ -848,6 +891,8 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     for (int s = 0; s < n_streams; s++) {
         const int32_t fl = states ? states[s].flags : 0;
         if (fl & ~(PAC_STREAM_HAS_PRIOR | PAC_STREAM_NO_FLUSH)) return set_err(PAC_E_ARG, "stream %d: flags", s);
+        if (fl && p->block_switch)        // a frame's window depends on the next frame's hop
+            return set_err(PAC_E_UNSUPPORTED, "block switching encodes whole streams (no continuation flags)");
         int64_t n = frame_offsets[s + 1] - frame_offsets[s];
         if (fl & PAC_STREAM_HAS_PRIOR) {   // a short prior is zero-padded, as the last hop (pcmfile.py:77-79)
             lead[s] = PAC_HALFN;
@@ -949,6 +994,8 @@ extern "C" int pac_encode_block(pac_ctx* c, const pac_params* p, const double* f
     int rc;
     if (!c || !full_block || !out || !out_bytes) return set_err(PAC_E_ARG, "null argument");
     if ((rc = check_params(p))) return rc;
+    if (p->block_switch)      // a frame's window depends on its neighbours' hops
+        return set_err(PAC_E_UNSUPPORTED, "block switching needs whole streams (pac_encode_streams)");
     const bool master = p->profile == PAC_PROFILE_MASTER;
     if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
     HIPCHK(hipSetDevice(c->device));
@@ -1249,7 +1296,8 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     const int64_t G1 = G > 0 ? G : 1;
     if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(G1 * PAC_HALFN)) ||
         (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
-        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)))
+        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)) ||
+        (p->block_switch && (rc = c->dec_bsf.ensure(G1))))
         return rc;
     HIPCHK(hipMemsetAsync(c->dec_err.p, 0, sizeof(int), s));
     HIPCHK(hipMemcpyAsync(c->dec_cbbase.p, cbb.data(), (n_streams + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
@@ -1278,7 +1326,8 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     if (G) {
         hipLaunchKernelGGL(k_dec_index, dim3((n_streams + 255) / 256), dim3(256), 0, s, ddev, c->dec_so.p, n_streams,
                            c->dec_cbbase.p, c->dec_cboff.p);
-        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p, c->dec_err.p};
+        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p, c->dec_err.p,
+                     p->block_switch ? c->dec_bsf.p : nullptr};
         hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, ddev, c->dec_cboff.p, G,
                            (int)master, T, master ? c->hdec_tab.p : nullptr, c->hdec, D);
         HIPCHK(hipGetLastError());

@@ -56,6 +56,13 @@ struct PacTables {
     // factored masking sums (pac_wave.h): 2^(KL z_l) and 2^(-KL z_l) per line,
     // KL = -27 log2(10)/10 as the device rounds it, evaluated in long double
     double pow_kl[PAC_HALFN], pow_mkl[PAC_HALFN];
+    // block-switching extension (pac_bs.h): the short transform (N = 512,
+    // 256 lines), its window, and the masking model's tables at N = 512
+    double sine_s[512];               // short MDCT window (sine, or KBD alpha 4)
+    double hann_s[512];
+    double2 mdct_pre_s[128];          // exp(-i pi (q+1/4)/256)
+    double2 mdct_post_s[128];         // exp(-i pi q / 256)
+    double bark_line_s[256], tiq_s[256], bark_bin_s[256], mld_s[256];
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

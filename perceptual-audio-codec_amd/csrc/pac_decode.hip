@@ -19,6 +19,7 @@
 //                              overlap-add, int16 conversion
 #include "pac_wave.h"
 #include "pac_kernels.h"
+#include "pac_bs.h"
 
 // Two-level Huffman decoding tables (built on the host in pac_huffman_load):
 // level 1 indexed by the first l1 bits of the next maxlen bits; an entry is
@@ -144,6 +145,7 @@ struct PacDecWork {
     uint8_t* overall;
     uint8_t* lrms;
     int* err;           // set to 1 when a channel-block's fields run past its nBytes
+    uint8_t* bsf;       // [G] block switching (pac_bs.h): the short-frame bit, or null: off
 };
 
 __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ data,
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
     }
     if (master)
         for (int b = 0; b < PAC_NB; ++b) D.lrms[g * PAC_NB + b] = (uint8_t)r.read(1);
+    if (D.bsf) D.bsf[g] = (uint8_t)r.read(1);
     if (bits_consumed(r, p + 4) > 8 * (int64_t)nbytes) atomicOr(D.err, 1);
 }
 
@@ -234,9 +237,26 @@ __device__ __forceinline__ void grp_dequant(const PacTables* __restrict__ T, con
 // IMDCT (mdct.py:72-79) of the lines in L, sine-windowed: w(n) for n < 2048
 // from U = 2 DCT-IV(L) (in buf):  n < 512: U[n+512];  512 <= n < 1536:
 // -U[1535-n];  n >= 1536: -U[n-1536]
-__device__ __forceinline__ double imdct_window_at(const double* U, const PacTables* __restrict__ T, int n) {
+__device__ __forceinline__ double imdct_window_at(const double* U, const PacTables* __restrict__ T, int n,
+                                                  int fl) {
     const double y = n < 512 ? U[n + 512] : (n < 1536 ? -U[1535 - n] : -U[n - 1536]);
-    return y * T->sine[n];
+    return y * (fl ? bs_long_win(T, fl, n) : T->sine[n]);
+}
+
+// Block switching (pac_bs.h): sample p < 2048 of a short frame's synthesis,
+// 0 + the windowed IMDCTs (N = 512) of the short blocks covering p in block
+// order; Uc[4 j + k] = U_k[j] = 2 DCT-IV of block k's lines.
+__device__ __forceinline__ double short_synth_at(const double* Uc, const PacTables* __restrict__ T, int p) {
+    double y = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int n = p - 384 - 256 * k;
+        if (n < 0 || n >= PAC_NS) continue;
+        const int j = n < 128 ? n + 128 : (n < 384 ? 383 - n : n - 384);
+        const double u = n < 128 ? Uc[4 * j + k] : -Uc[4 * j + k];
+        y = y + u * T->sine_s[n];
+    }
+    return y;
 }
 
 // one synthesis workgroup: blocks [b0, b1) of stream s, channels c0 .. c0+nc-1
@@ -293,13 +313,37 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
             }
             __syncthreads();
         }
+        // block switching: this frame short, or a long frame's start / stop shape
+        int fl = 0;
+        if (D.bsf) {
+            const int64_t g0 = cb_base[s] + b * nch;
+            fl = (D.bsf[g0] ? PAC_BS_SHORT : 0) | (b > 0 && D.bsf[g0 - nch] ? PAC_BS_PREV : 0) |
+                 (b + 1 < nb && D.bsf[g0 + nch] ? PAC_BS_NEXT : 0);
+        }
         for (int c = 0; c < nc; ++c) {
-            const double* U = grp_dct4<256>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
+            const double* U;
+            if (fl & PAC_BS_SHORT) {      // wave k: U_k = 2 DCT-IV of block k, back into its line slots
+                const int k = tid / WAVE;
+                double* Lc = lines[c];
+                wave_dct4_256([&](int j) { return Lc[4 * j + k]; }, T, buf + 256 * k, tid & (WAVE - 1), 2.0,
+                              [&](int j, double v) { Lc[4 * j + k] = v; });
+                __syncthreads();
+                U = Lc;
+            } else {
+                U = grp_dct4<256>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
+            }
             const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
 #pragma unroll
             for (int i0 = 0; i0 < PAC_HALFN; i0 += 256) {
                 const int i = i0 + tid;
-                const double w0 = imdct_window_at(U, T, i), w1 = imdct_window_at(U, T, i + PAC_HALFN);
+                double w0, w1;
+                if (fl & PAC_BS_SHORT) {
+                    w0 = short_synth_at(U, T, i);
+                    w1 = short_synth_at(U, T, i + PAC_HALFN);
+                } else {
+                    w0 = imdct_window_at(U, T, i, fl);
+                    w1 = imdct_window_at(U, T, i + PAC_HALFN, fl);
+                }
                 if (b >= b0 && b >= 1 - (O.preroll ? 1 : 0)) {
                     const double v = prev[c][i] + w0;
                     const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;

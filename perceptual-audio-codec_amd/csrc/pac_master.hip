@@ -24,6 +24,8 @@
 // The tail of chunk i runs on a second HIP stream, concurrently with the
 // threshold/front kernels of chunk i+1 (double-buffered chunk outputs).
 
+#include "pac_bs.h"
+
 // chunk-local scratch, local block j (thr single-buffered: written and read on
 // the front stream; the rest double-buffered between front and tail)
 struct PacMasterChunkBuf {
@@ -46,6 +48,7 @@ struct PacMasterFields {
     uint32_t* dbg_mant;  // [G][1024]
     uint64_t* dbg_code;  // [G][1024]
     uint8_t* dbg_len;    // [G][1024]
+    const uint8_t* bsf;  // [nblocks] PAC_BS_* flags (block-switching extension), or null: off
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of streams
@@ -71,13 +74,16 @@ __device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off,
 // LRMS-variant signals: the in-place window chains of EncodeDualChannel and
 // getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
 // M = (a+b)/2, S = (a-b)/2; v2 = M*hann, v3 = S*hann, v4 = (M*hann)*hann, ...
+// fl: block-switching flags of a long frame (the MDCT window's start / stop
+// shapes, pac_bs.h), 0 = the plain window
 __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const BlockPcm& rR,
-                                                 const PacTables* __restrict__ T, int v, int i) {
+                                                 const PacTables* __restrict__ T, int v, int i, int fl) {
     const double h = T->hann[i];
-    if (v == 1) return __dmul_rn(__dmul_rn(rR(i), T->sine[i]), h);
-    const double a = __dmul_rn(__dmul_rn(rL(i), T->sine[i]), h);
+    const double w = fl ? bs_long_win(T, fl, i) : T->sine[i];
+    if (v == 1) return __dmul_rn(__dmul_rn(rR(i), w), h);
+    const double a = __dmul_rn(__dmul_rn(rL(i), w), h);
     if (v == 0) return a;
-    const double b = __dmul_rn(__dmul_rn(rR(i), T->sine[i]), h);
+    const double b = __dmul_rn(__dmul_rn(rR(i), w), h);
     double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
     ms = __dmul_rn(ms, h);
     if (v >= 4) ms = __dmul_rn(ms, h);
@@ -98,6 +104,8 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int v = (int)(item % nvar);
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;     // uniform per workgroup
+    const int fl = F.bsf ? F.bsf[gb] : 0;
+    if (fl & PAC_BS_SHORT) return;                          // k_master_thr_short's
     // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
     // the M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
     // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
@@ -121,7 +129,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     if (!rows) return;                                      // uniform per workgroup
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
-    auto d = [&](int i) { return variant_sample(rL, rR, T, v, i); };
+    auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
     const MaskerLists L = masker_lists(buf, tmp, rank);
     const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
@@ -140,6 +148,94 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
         out[r * WAVE + lane] = wave_masking_row(L, nm, T, lane, r);
     }
+}
+
+// Block-switching extension (pac_bs.h): the thresholds of a SHORT frame.  One
+// 256-thread workgroup per (block, variant), wave k = short block k: the
+// variant's in-place window chain on the block's 512 samples (short window,
+// Hann, M/S as variant_sample), calcBTHR at N = 512, written interleaved
+// (line 4 j + k) where the long thresholds go.
+__global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const PacTables* __restrict__ T,
+                                                          PacMasterChunkBuf K, PacMasterFields F,
+                                                          PacMasterChunk ck) {
+    __shared__ double2 bufs[4][2][256];                     // per wave: FFT buffer + scratch (32 KB)
+    __shared__ double pw[4][256];
+    __shared__ double mz[4][128], mS[4][128], mlev[4][128];
+    __shared__ int kidx[4][128];
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), k = tid / WAVE;
+    const int64_t item = xcd_item(blockIdx.x, gridDim.x);
+    const int nvar = ck.nch == 2 ? 6 : 1;
+    const int64_t j = item / nvar;
+    const int v = (int)(item % nvar);
+    int64_t gb;
+    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    if (!(F.bsf[gb] & PAC_BS_SHORT)) return;
+    const BlockPcm rL(locate(src, gb, 0));
+    const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));
+    const int o = 384 + 256 * k;
+    auto d = [&](int i) {
+        const double h = T->hann_s[i], w = T->sine_s[i];
+        if (v == 1) return __dmul_rn(__dmul_rn(rR(o + i), w), h);
+        const double a = __dmul_rn(__dmul_rn(rL(o + i), w), h);
+        if (v == 0) return a;
+        const double b = __dmul_rn(__dmul_rn(rR(o + i), w), h);
+        double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
+        ms = __dmul_rn(ms, h);
+        if (v >= 4) ms = __dmul_rn(ms, h);
+        return ms;
+    };
+    wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw[k], lane);
+    double* out = K.thr + (j * 6 + v) * PAC_HALFN;
+    wave_threshold_short(pw[k], T, v >= 4 ? 0.0 : 15.0, mz[k], mS[k], mlev[k], kidx[k], lane,
+                         [&](int l, double t) { out[4 * l + k] = t; });
+}
+
+// Block switching: attack flags, one wave per two blocks.  Lane (b, c, s)
+// sums the first-difference energy of segment s (128 samples) of channel c
+// of block b in sample order; the lanes of the new half's segments compare
+// it with the mean of the 8 segments before it (pac_bs.h).
+__global__ __launch_bounds__(64) void k_bs_attack(PacSource src, int64_t nblocks, uint8_t* __restrict__ att) {
+    __shared__ double E[2][2][16];
+    const int lane = threadIdx.x;
+    const int b2 = lane >> 5, c = (lane >> 4) & 1, sg = lane & 15;
+    const int64_t gb = (int64_t)blockIdx.x * 2 + b2;
+    const bool live = gb < nblocks && c < src.n_ch;
+    double e = 0.0;
+    if (live) {
+        const BlockPcm r(locate(src, gb, c));
+        double xp = sg ? r(128 * sg - 1) : 0.0;
+        for (int n = 128 * sg; n < 128 * sg + 128; ++n) {
+            const double x = r(n);
+            const double dd = n ? __dsub_rn(x, xp) : 0.0;
+            e = __dadd_rn(e, __dmul_rn(dd, dd));
+            xp = x;
+        }
+    }
+    E[b2][c][sg] = e;
+    wave_sync();
+    bool a = false;
+    if (live && sg >= 8) {
+        double m = 0.0;
+        for (int q = sg - 8; q < sg; ++q) m = __dadd_rn(m, E[b2][c][q]);
+        a = e > PAC_BS_RATIO * (m / 8.0) && e > PAC_BS_EMIN;
+    }
+    const unsigned long long bal = __ballot(a);
+    if (gb < nblocks && (lane & 31) == 0) att[gb] = ((bal >> (32 * b2)) & 0xffffffffull) ? 1 : 0;
+}
+
+// Block switching: per block PAC_BS_* from the attack flags of its stream
+// (short: an attack in it or the block before; PREV / NEXT: the neighbour's)
+__global__ void k_bs_flags(const int64_t* __restrict__ blk_off, int n_streams, int64_t nblocks,
+                           const uint8_t* __restrict__ att, uint8_t* __restrict__ fl) {
+    const int64_t gb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gb >= nblocks) return;
+    int lo = 0, hi = n_streams;                 // stream: last s with blk_off[s] <= gb
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (blk_off[mid] <= gb) lo = mid; else hi = mid; }
+    const int64_t t = gb - blk_off[lo], len = blk_off[lo + 1] - blk_off[lo];
+    const bool sh = att[gb] || (t > 0 && att[gb - 1]);
+    const bool pv = t > 0 && (att[gb - 1] || (t > 1 && att[gb - 2]));
+    const bool nx = t + 1 < len && (att[gb + 1] || att[gb]);
+    fl[gb] = (uint8_t)((sh ? PAC_BS_SHORT : 0) | (pv ? PAC_BS_PREV : 0) | (nx ? PAC_BS_NEXT : 0));
 }
 
 // --- numpy pairwise summation of a complex vector (loops_utils.h.src) -------
@@ -275,6 +371,8 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     const bool st = ck.nch == 2;                 // mono master: channel 0 alone, LRMS all 0
+    const int fl = F.bsf ? F.bsf[gb] : 0;        // block-switching flags (pac_bs.h), 0: off
+    const bool sh = fl & PAC_BS_SHORT;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, st ? 1 : 0));
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
@@ -282,9 +380,22 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     __syncthreads();
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
-    const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-    const double* XR = st ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
-                          : nullptr;
+    const double* XL;
+    const double* XR = nullptr;
+    if (sh) {          // four short MDCTs per channel, interleaved (scratch: the buffers' upper halves)
+        double* xl = reinterpret_cast<double*>(bufA);
+        double* xr = reinterpret_cast<double*>(bufB);
+        grp_short_mdct(rL, T, bufA + 512, bufB + 512, xl, tid);
+        if (st) grp_short_mdct(rR, T, bufA + 512, bufB + 512, xr, tid);
+        XL = xl;
+        XR = xr;
+    } else if (fl) {   // long frame next to a short one: start / stop window
+        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
+        if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid);
+    } else {
+        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
+        if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
+    }
     double xl4[4], xr4[4];
     double mL = 0.0, mR = 0.0;
 #pragma unroll
@@ -321,7 +432,7 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         if (ms) {
             const double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
             const double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
-            const double mld = T->mld[l];
+            const double mld = sh ? T->mld_s[l >> 2] : T->mld[l];
             const double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
             const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
             const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
@@ -540,7 +651,7 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
             dep_add += (long)orig - ((long)best + nsign + 4);
             if (q == 0) {
                 F.tid[g] = (uint8_t)bestid;
-                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + 7) / 8;
+                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
             }
             wave_sync();                               // ba_s / sf_s rewritten by the next channel
         }
@@ -549,10 +660,10 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
     if (q == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
 }
 
-// worst-case master channel-block: 8 + 25 * 8 + 25 bits + per line one sign bit
-// and a code of at most max(code length, escape length + ba) <= 30 + 16 bits
-// (pac_huffman_load rejects longer codes)
-#define PAC_MASTER_MAX_BITS (8 + PAC_NB * 8 + PAC_NB + PAC_HALFN * (1 + 30 + 16))
+// worst-case master channel-block: 8 + 25 * 8 + 25 (+ 1 block-switching) bits
+// + per line one sign bit and a code of at most max(code length, escape
+// length + ba) <= 30 + 16 bits (pac_huffman_load rejects longer codes)
+#define PAC_MASTER_MAX_BITS (8 + PAC_NB * 8 + PAC_NB + 1 + PAC_HALFN * (1 + 30 + 16))
 #define PACK_WORDS_MASTER ((PAC_MASTER_MAX_BITS + 31) / 32)
 static_assert(PACK_WORDS_MASTER * 4 <= 16384, "packed words must fit a 16 KB line buffer");
 
@@ -600,9 +711,25 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         bas[cc][b] = F.ba[(gb * nch + cc) * PAC_NB + b];
         sfs[cc][b] = F.sf[(gb * nch + cc) * PAC_NB + b];
     }
-    const double* XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-    const double* XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
-                                : XL;
+    const int fl = F.bsf ? F.bsf[gb] : 0;     // block-switching flags (pac_bs.h), 0: off
+    const double* XL;
+    const double* XR;
+    if (fl & PAC_BS_SHORT) {                   // as k_master_front: the interleaved short MDCTs
+        double* xl = reinterpret_cast<double*>(bufA);
+        double* xr = reinterpret_cast<double*>(bufB);
+        grp_short_mdct(rL, T, bufA + 512, bufB + 512, xl, tid);
+        if (nch == 2) grp_short_mdct(rR, T, bufA + 512, bufB + 512, xr, tid);
+        XL = xl;
+        XR = nch == 2 ? xr : xl;
+    } else if (fl) {
+        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
+        XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid)
+                      : XL;
+    } else {
+        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
+        XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
+                      : XL;
+    }
     const double gL = (double)(1 << F.overall[gb * nch]);
     const double gR = nch == 2 ? (double)(1 << F.overall[gb * 2 + 1]) : gL;
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
@@ -703,6 +830,8 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         }
     } else if (lane < PAC_NB) {
         put_bits(wd, bstart[c][PAC_NB] + tot_bits[c] + lane, (uint32_t)lr[lane], 1);
+    } else if (lane == PAC_NB && F.bsf) {     // block switching: the short-frame bit
+        put_bits(wd, bstart[c][PAC_NB] + tot_bits[c] + PAC_NB, (uint32_t)(fl & PAC_BS_SHORT), 1);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {

@@ -137,7 +137,7 @@ class PACFile(AudioFile):
 # ---------------------------------------------------------------------------
 
 def encode_streams(streams, sample_rate, profile=PROFILE_MASTER, context=None, states=None,
-                   window=_lib.WINDOW_SINE):
+                   window=_lib.WINDOW_SINE, block_switch=False):
     """Encode independent streams (list of int16 [frames, nCh] arrays sharing
     sample rate and channel count).  Returns a list of data-section bytes."""
     ctx = context or codec.default_context()
@@ -146,7 +146,7 @@ def encode_streams(streams, sample_rate, profile=PROFILE_MASTER, context=None, s
     fo[1:] = np.cumsum([s.shape[0] for s in streams])
     pcm = np.concatenate([np.ascontiguousarray(s, dtype=np.int16) for s in streams]) \
         if len(streams) > 1 else np.ascontiguousarray(streams[0], dtype=np.int16)
-    p = _lib.params(sample_rate, nch, profile, window=window)
+    p = _lib.params(sample_rate, nch, profile, window=window, block_switch=block_switch)
     out, so = ctx.encode_streams(p, pcm, fo, states=states)
     return [out[so[i]:so[i + 1]].tobytes() for i in range(len(streams))]
 
@@ -169,11 +169,11 @@ def encode_stream_parts(frames, sample_rate, parts, profile=PROFILE_MASTER, cont
     return body
 
 
-def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE):
+def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE, block_switch=False):
     """The reference driver's encode half (pacfile.py:430-499) for one file,
     as a single GPU call.  Returns the coded file bytes (and writes them)."""
     cp, frames = read_for_encode(in_path)
-    body = encode_streams([frames], cp.sampleRate, profile, context, window=window)[0]
+    body = encode_streams([frames], cp.sampleRate, profile, context, window=window, block_switch=block_switch)[0]
     data = header_bytes(cp.sampleRate, cp.nChannels, cp.numSamples) + body
     if out_path:
         with open(out_path, "wb") as f:
@@ -182,7 +182,7 @@ def encode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, wi
 
 
 def encode_wav_files(wav_files, profile=PROFILE_MASTER, context=None, n_channels=None, sample_rate=None,
-                     window=_lib.WINDOW_SINE):
+                     window=_lib.WINDOW_SINE, block_switch=False):
     """The encode driver (pacfile.py:430-499) for many WAV files (paths or
     bytes) sharing sample rate and channel count, with the WAV parsing on the
     device (pac_encode_wav).  Returns the coded files' bytes."""
@@ -201,7 +201,7 @@ def encode_wav_files(wav_files, profile=PROFILE_MASTER, context=None, n_channels
         first = ctx.wav_scan(blobs[0], [0, len(blobs[0])])[0]
         sample_rate = sample_rate or first.sample_rate
         n_channels = n_channels or first.n_channels
-    p = _lib.params(sample_rate, n_channels, profile, window=window)
+    p = _lib.params(sample_rate, n_channels, profile, window=window, block_switch=block_switch)
     out, so, info = ctx.encode_wav(p, blob, fo)
     return [header_bytes(w.sample_rate, w.n_channels, w.num_samples) + out[so[i]:so[i + 1]].tobytes()
             for i, w in enumerate(info)]
@@ -223,7 +223,7 @@ def parse_header(b):
 
 
 def decode_streams(sections, sample_rate, n_channels, profile=PROFILE_MASTER, context=None, preroll=False,
-                   window=_lib.WINDOW_SINE):
+                   window=_lib.WINDOW_SINE, block_switch=False):
     """Decode independent data sections (bytes) sharing sample rate and channel
     count in one GPU call.  Returns a list of int16 [frames, nCh] arrays: the
     frames the reference's decode driver writes (or, with preroll, every
@@ -231,7 +231,7 @@ def decode_streams(sections, sample_rate, n_channels, profile=PROFILE_MASTER, co
     ctx = context or codec.default_context()
     so = np.zeros(len(sections) + 1, dtype=np.int64)
     so[1:] = np.cumsum([len(x) for x in sections])
-    p = _lib.params(sample_rate, n_channels, profile, window=window)
+    p = _lib.params(sample_rate, n_channels, profile, window=window, block_switch=block_switch)
     pcm, fo, _ = ctx.decode_streams(p, b"".join(sections), so, preroll=preroll)
     return [pcm[fo[i]:fo[i + 1]] for i in range(len(sections))]
 
@@ -245,13 +245,13 @@ def wav_bytes(sampleRate, nChannels, numSamples, frames):
     return h + np.ascontiguousarray(frames, dtype="<i2").tobytes()
 
 
-def decode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE):
+def decode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE, block_switch=False):
     """The reference driver's decode half (pacfile.py:430-499) for one coded
     file, as one GPU call.  Returns the output WAV bytes (and writes them)."""
     with open(in_path, "rb") as f:
         b = f.read()
     fs, nch, ns, _, off = parse_header(b)
-    pcm = decode_streams([b[off:]], fs, nch, profile, context, window=window)[0]
+    pcm = decode_streams([b[off:]], fs, nch, profile, context, window=window, block_switch=block_switch)[0]
     out = wav_bytes(fs, nch, ns, pcm)
     if out_path:
         with open(out_path, "wb") as f:
@@ -259,7 +259,7 @@ def decode_file(in_path, out_path=None, profile=PROFILE_MASTER, context=None, wi
     return out
 
 
-def decode_to_wav(coded_files, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE):
+def decode_to_wav(coded_files, profile=PROFILE_MASTER, context=None, window=_lib.WINDOW_SINE, block_switch=False):
     """The decode driver (pacfile.py:430-499) for many coded files (bytes)
     sharing sample rate and channel count: the output WAV files' bytes, the
     WAV header and sample conversion written on the device (pac_decode_wav)."""
@@ -269,6 +269,6 @@ def decode_to_wav(coded_files, profile=PROFILE_MASTER, context=None, window=_lib
     secs = [b[h[4]:] for b, h in zip(coded_files, heads)]
     so = np.zeros(len(secs) + 1, dtype=np.int64)
     so[1:] = np.cumsum([len(x) for x in secs])
-    p = _lib.params(fs, nch, profile, window=window)
+    p = _lib.params(fs, nch, profile, window=window, block_switch=block_switch)
     out, wo = ctx.decode_wav(p, b"".join(secs), so, [h[2] for h in heads])
     return [out[wo[i]:wo[i + 1]].tobytes() for i in range(len(secs))]

@@ -15,6 +15,11 @@ Workloads (BASELINE.json configs; --config picks one, default 2):
      tests/fixtures/inputs/) x --copies, each copy an independent master +
      Huffman stream (per-file reservoir exactly as the reference), whole
      streams sharded over the ranks by pac_amd.shard.plan (LPT).
+  4  block switching (an extension, parity unpinned -- pac_bs.h): synthetic
+     48 kHz stereo pink noise + tones + one decaying noise burst per 8192
+     frames, N=1024/256 block switching with attack detection, master
+     profile; 1.25 x 10^7 stereo blocks per GPU (12 500 streams x 1000
+     blocks), i.e. 10^8 over the 8 GPUs of configs[4].
 
 The PCM is generated on (configs 1-2) or uploaded to (config 3) the device
 before the timed region, so the timed region starts with the inputs resident
@@ -56,9 +61,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, choices=[1, 2, 3], default=2,
+    ap.add_argument("--config", type=int, choices=[1, 2, 3, 4], default=2,
                     help="BASELINE.json configs[i]: 1 origin white noise 10^6, 2 master pink+tones 10^7 "
-                         "(default), 3 master real-audio file batch")
+                         "(default), 3 master real-audio file batch, 4 block switching 1.25x10^7 per GPU")
     ap.add_argument("--mode", choices=["encode", "decode"], default="encode",
                     help="encode = the metric (default); decode = pac_decode_streams of the same "
                          "workload's bitstream (encoded once, untimed)")
@@ -78,9 +83,10 @@ def parse():
     if a.profile is not None:
         a.config = 1 if a.profile == "origin" else 2
     a.master = a.config != 1
+    a.bs = a.config == 4
     a.profile = "master" if a.master else "origin"
     if a.streams is None:
-        a.streams = 10000 if a.config == 2 else 1000
+        a.streams = {2: 10000, 4: 12500}.get(a.config, 1000)
     return a
 
 
@@ -160,7 +166,7 @@ def measured_profile(kind, kernel):
     return out, rel
 
 
-def cpu_baseline(ctx, samples, fs, seconds, profile, threads):
+def cpu_baseline(ctx, samples, fs, seconds, profile, threads, bs=False):
     """The CPU oracle (oracle/pac_oracle.c) on a bounded sample of the same
     workload, one host thread per stream (ctypes releases the GIL; the C
     oracle keeps no global state): thread t encodes growing prefixes of its
@@ -175,7 +181,7 @@ def cpu_baseline(ctx, samples, fs, seconds, profile, threads):
     t0 = time.perf_counter()
 
     def work(t):
-        o = P.Oracle(fs, huffman=(prof == P.MASTER))
+        o = P.Oracle(fs, huffman=(prof == P.MASTER), block_switch=bs)
         pcm = samples[t]
         full = (pcm.shape[0] + 1023) // 1024 + 1
         done, chunk, last = 0, 16, b""
@@ -194,8 +200,9 @@ def cpu_baseline(ctx, samples, fs, seconds, profile, threads):
     done = sum(r[0] for r in res)
     base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
-                      "fixtures), %s profile, %d host threads (one stream each, growing prefixes), "
-                      "%d stereo blocks of the same streams in %.1f s" % (profile, threads, done, el)}
+                      "fixtures), %s profile%s, %d host threads (one stream each, growing prefixes), "
+                      "%d stereo blocks of the same streams in %.1f s"
+                      % (profile, " + block switching" if bs else "", threads, done, el)}
     return base, [r[1] for r in res]
 
 
@@ -301,10 +308,12 @@ def synthetic_job(a, ctx, rank):
     fps = (a.blocks_per_stream - 1) * 1024
     n_frames = a.streams * fps
     fo = np.arange(a.streams + 1, dtype=np.int64) * fps
-    p = _lib.params(fs, 2, 1 if a.master else 0)
+    p = _lib.params(fs, 2, 1 if a.master else 0, block_switch=a.bs)
     pcm_dev = ctx.alloc(n_frames * 2 * 2)
     if a.master:
         ctx.synth_pink_tones(pcm_dev, n_frames, fs, seed=1234 + 7919 * rank)
+        if a.bs:
+            ctx.synth_bursts(pcm_dev, n_frames, 8192, seed=99 + 7919 * rank)
     else:
         ctx.synth_white(pcm_dev, n_frames * 2, seed=1234 + 7919 * rank)
     return [Job(ctx, p, fo, pcm_dev)]
@@ -498,7 +507,7 @@ def main():
     dom_s = kern_ms[dom] / 1e3
     alg_bytes = blocks * ALG_BYTES.get(dom, 4096)
     achieved = alg_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
-    prof, prof_note = measured_profile(a.profile, dom)
+    prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
     traffic = None
     ref_flop = REF_ALG_FLOP_PER_BLOCK[a.profile]
     step_s = el_max / a.steps
@@ -520,6 +529,13 @@ def main():
         workload = ("BASELINE configs[2]: synthetic 48 kHz stereo pink noise + tones, %d stereo blocks per GPU "
                     "(%d streams x %d blocks), N=1024 MDCT, full psychoacoustics + M/S + bit allocation + "
                     "Huffman (master profile)" % (blocks, a.streams, a.blocks_per_stream))
+    elif a.config == 4:
+        data = ("synthetic (device-generated pink noise + 440/1250/5300 Hz tones + one decaying "
+                "gaussian noise burst per 8192 frames at a hashed onset)")
+        workload = ("BASELINE configs[4]: block switching N=1024/256 with attack detection (extension, parity "
+                    "unpinned: byte-exact vs the oracle's restatement), synthetic 48 kHz stereo, %d stereo "
+                    "blocks per GPU (%d streams x %d blocks; 10^8 at 8 GPUs), master profile"
+                    % (blocks, a.streams, a.blocks_per_stream))
     elif a.config == 1:
         data = "synthetic (device-generated white noise, counter-hash Box-Muller)"
         workload = ("BASELINE configs[1]: synthetic 48 kHz stereo white noise, %d stereo blocks per GPU "
@@ -568,7 +584,8 @@ def main():
         nt = max(1, min(a.cpu_threads, j.ns))
         samples = j.cpu_samples(nt)
         starts = [int(j.so[t]) for t in range(len(samples))]
-        res["cpu_baseline"], prefixes = cpu_baseline(ctx, samples, j.p.sample_rate, a.cpu_seconds, a.profile, nt)
+        res["cpu_baseline"], prefixes = cpu_baseline(ctx, samples, j.p.sample_rate, a.cpu_seconds, a.profile, nt,
+                                                     bs=a.bs)
         res["parity"] = parity_check(ctx, j.out_dev, starts, prefixes)
     for j in jobs:
         j.free()

@@ -231,6 +231,9 @@ int pac_synth_white(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_samples, uint64_t 
  * n_frames interleaved L/R frames. */
 int pac_synth_pink_tones(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_frames, int32_t sample_rate,
                          uint64_t seed);
+/* Decaying noise bursts (one per `period` frames, hashed onset) added in place
+ * to stereo PCM: the transients of the block-switching workload (configs[4]). */
+int pac_synth_bursts(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_frames, int64_t period, uint64_t seed);
 int pac_sync(pac_ctx *ctx);
 int pac_set_timing(pac_ctx *ctx, int32_t enable);
 /* Stereo blocks per master-profile chunk (device scratch ~65 KB/block). */

@@ -109,6 +109,7 @@ def lib():
         "pac_copy_to_host": (C.c_int, [vp, vp, vp, i64]),
         "pac_synth_white": (C.c_int, [vp, vp, i64, C.c_uint64]),
         "pac_synth_pink_tones": (C.c_int, [vp, vp, i64, C.c_int32, C.c_uint64]),
+        "pac_synth_bursts": (C.c_int, [vp, vp, i64, i64, C.c_uint64]),
         "pac_sync": (C.c_int, [vp]),
         "pac_set_timing": (C.c_int, [vp, i32]),
         "pac_set_chunk_blocks": (C.c_int, [vp, i64]),
@@ -335,6 +336,9 @@ class Context:
 
     def synth_pink_tones(self, dev_pcm, n_frames, sample_rate, seed):
         check(self.L.pac_synth_pink_tones(self.h, dev_pcm, int(n_frames), int(sample_rate), int(seed)))
+
+    def synth_bursts(self, dev_pcm, n_frames, period, seed):
+        check(self.L.pac_synth_bursts(self.h, dev_pcm, int(n_frames), int(period), int(seed)))
 
     def debug_threshold(self, sample_rate, data, no_drop=False):
         d = np.ascontiguousarray(np.atleast_2d(data), dtype=np.float64)

@@ -1142,6 +1142,14 @@ extern "C" int pac_synth_pink_tones(pac_ctx* c, int16_t* dev_pcm, int64_t n_fram
     HIPCHK(hipStreamSynchronize(c->stream));
     return PAC_OK;
 }
+
+extern "C" int pac_synth_bursts(pac_ctx* c, int16_t* dev_pcm, int64_t n_frames, int64_t period, uint64_t seed) {
+    if (!c || !dev_pcm || n_frames < 0 || period < 4096) return set_err(PAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_synth_bursts, dim3(4096), dim3(256), 0, c->stream, dev_pcm, n_frames, period, seed);
+    HIPCHK(hipGetLastError());
+    return PAC_OK;
+}
 extern "C" int pac_sync(pac_ctx* c) {
     if (!c) return set_err(PAC_E_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->device));

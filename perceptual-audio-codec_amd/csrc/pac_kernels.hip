@@ -583,3 +583,31 @@ __global__ void k_synth_pink_tones(int16_t* __restrict__ pcm, int64_t n_frames, 
         }
     }
 }
+
+// synthetic configs[4] input (bench, block switching): decaying noise bursts
+// added in place to stereo interleaved PCM.  One burst per period of `period`
+// frames, its onset at a hashed offset in [0, period - 2560); burst sample at
+// d frames after the onset = gaussian(hash) * env, env = exp(-d / 500) over
+// 2560 frames, amplitude 0.4 (L) / 0.3 (R) of full scale; saturating int16.
+__global__ void k_synth_bursts(int16_t* __restrict__ pcm, int64_t n_frames, int64_t period, uint64_t seed) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (; i < n_frames; i += stride) {
+        const int64_t per = i / period;
+        const int64_t t0 = per * period + (int64_t)(splitmix64(seed ^ 0x9e3779b97f4a7c15ull ^ (uint64_t)per) %
+                                                    (uint64_t)(period - 2560));
+        const int64_t d = i - t0;
+        if (d < 0 || d >= 2560) continue;
+        const double env = exp(-(double)d / 500.0);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint64_t h1 = splitmix64(seed ^ (4 * (uint64_t)i + 2 * c));
+            const uint64_t h2 = splitmix64(seed ^ (4 * (uint64_t)i + 2 * c + 1));
+            const double u1 = ((double)(h1 >> 11) + 1.0) * 0x1.0p-53, u2 = (double)(h2 >> 11) * 0x1.0p-53;
+            const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+            double x = (double)pcm[2 * i + c] + __builtin_rint(z * (c ? 0.3 : 0.4) * 32767.0 * env);
+            x = x > 32767.0 ? 32767.0 : (x < -32768.0 ? -32768.0 : x);
+            pcm[2 * i + c] = (int16_t)x;
+        }
+    }
+}

@@ -318,6 +318,8 @@ struct pac_ctx {
     DevBuf<uint8_t> bs_att, bs_fl;          // block switching: attack / PAC_BS_* flags per block
     DevBuf<uint8_t> dec_bsf;                // decoder: the short-frame bit per channel-block
     hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
+    hipStream_t stream3 = nullptr;          // master: the LRMS decisions, running ahead of the thresholds
+    bool lrms_async = true;                 // PAC_LRMS_ASYNC=0: LRMS in line on the front stream
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
     DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)
@@ -358,13 +360,15 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     pac_ctx* c = new pac_ctx();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
     }
     for (auto& e : c->ev) hipEventCreate(&e);
     for (auto& e : c->evs) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (const char* f = getenv("PAC_DEBUG_FLAGS")) c->dbg = atoi(f);
+    if (const char* f = getenv("PAC_LRMS_ASYNC")) c->lrms_async = atoi(f) != 0;
     *out = c;
     return PAC_OK;
 }
@@ -374,7 +378,9 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->stream2);
+    hipStreamSynchronize(c->stream3);
     for (auto& kv : c->tables) hipFree(kv.second);
+    c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
@@ -395,6 +401,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     for (auto& e : c->evs) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
     hipStreamDestroy(c->stream2);
+    hipStreamDestroy(c->stream3);
     delete c;
 }
 
@@ -775,24 +782,26 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         F.dbg_code = c->dbg_code.p;
         F.dbg_len = c->dbg_len.p;
     }
-    hipStream_t s0 = c->stream, s1 = c->stream2;
+    hipStream_t s0 = c->stream, s1 = c->stream2, s2 = c->stream3;
+    const bool lrms_async = c->lrms_async && nch == 2;
     const double budget = bit_budget(p);
     // timing: events recorded around every launch on its own stream, read
     // once after the call; mk[k] = (pool event, phase) of stream k, phase -1
     // opens an interval, phase >= 0 closes one
-    std::vector<std::pair<size_t, int>> mk[2];
+    std::vector<std::pair<size_t, int>> mk[3];
     size_t nev = 0;
     auto mark = [&](int k, int phase) -> int {
         if (!c->timing) return PAC_OK;
         const hipEvent_t e = c->pool_event(nev);
         mk[k].emplace_back(nev++, phase);
-        HIPCHK(hipEventRecord(e, k ? s1 : s0));
+        HIPCHK(hipEventRecord(e, k == 2 ? s2 : (k ? s1 : s0)));
         return PAC_OK;
     };
     // mono: the LRMS flags are all 0 (L/R coding; the 25 bits are still written)
     if (nch == 1) HIPCHK(hipMemsetAsync(c->m_lrms.p, 0, nblocks * PAC_NB, s0));
     HIPCHK(hipEventRecord(c->evs[4], s0));            // states and tables are on s0
     HIPCHK(hipStreamWaitEvent(s1, c->evs[4], 0));
+    if (lrms_async) HIPCHK(hipStreamWaitEvent(s2, c->evs[4], 0));
     int64_t i = 0;
     for (const Grp& gr : groups) {
         for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S, ++i) {
@@ -802,10 +811,22 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                                       c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB};
             const int64_t B = (int64_t)gr.n_s * gr.S;
             if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
-            if ((rc = mark(0, -1))) return rc;
-            if (nch == 2)
-                hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
-            if ((rc = mark(0, 5))) return rc;
+            if (lrms_async) {
+                // the LRMS decisions depend on the PCM alone: on their own stream,
+                // free to run ahead and fill the issue slots the thresholds leave
+                if ((rc = mark(2, -1))) return rc;
+                hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s2, src, T, F, ck);
+                if ((rc = mark(2, 5))) return rc;
+                const hipEvent_t ev = c->pool_event(nev++);
+                HIPCHK(hipEventRecord(ev, s2));
+                HIPCHK(hipStreamWaitEvent(s0, ev, 0));
+                if ((rc = mark(0, -1))) return rc;
+            } else {
+                if ((rc = mark(0, -1))) return rc;
+                if (nch == 2)
+                    hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
+                if ((rc = mark(0, 5))) return rc;
+            }
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
             if (F.bsf)     // the short frames' thresholds (the long kernel skips them)
                 hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(B * nvar)), dim3(256), 0, s0, src, T, K, F,
@@ -844,7 +865,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
         float ph[6] = {0, 0, 0, 0, 0, 0};
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < 3; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
                 float ms = 0.f;

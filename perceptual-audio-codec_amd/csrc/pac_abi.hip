@@ -311,6 +311,7 @@ struct pac_ctx {
     // master
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
+    DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack)
     DevBuf<int64_t> st_extra, st_deposit;
     DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
     DevBuf<uint64_t> dbg_code;
@@ -380,7 +381,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamSynchronize(c->stream2);
     hipStreamSynchronize(c->stream3);
     for (auto& kv : c->tables) hipFree(kv.second);
-    c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release();
+    c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
@@ -763,8 +764,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_lines.ensure(2 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(2 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(2 * cbmax * 2 * PAC_NB)))
         return rc;
+    if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
-                      nullptr, nullptr, nullptr, nullptr};
+                      nullptr, nullptr, nullptr, c->m_codes.p, nullptr};
     if (p->block_switch) {     // pac_bs.h: attack flags, then each block's PAC_BS_* flags
         if ((rc = c->bs_att.ensure(nblocks + 1)) || (rc = c->bs_fl.ensure(nblocks + 1))) return rc;
         hipLaunchKernelGGL(k_bs_attack, dim3((unsigned)((nblocks + 1) / 2)), dim3(64), 0, c->stream, src, nblocks,
@@ -857,7 +859,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                        c->off.p);
     HIPCHK(hipGetLastError());
     if ((rc = mark(0, 4))) return rc;
-    hipLaunchKernelGGL(k_master_pack, dim3((unsigned)nblocks), dim3(256), 0, s0, src, T, c->huff, F, nblocks,
+    hipLaunchKernelGGL(k_master_pack, dim3((unsigned)nblocks), dim3(256), 0, s0, T, c->huff, F, nch, nblocks,
                        c->off.p, out_dev, out_cap);
     HIPCHK(hipGetLastError());
     if ((rc = mark(0, 3))) return rc;

@@ -48,6 +48,7 @@ struct PacMasterFields {
     uint32_t* dbg_mant;  // [G][1024]
     uint64_t* dbg_code;  // [G][1024]
     uint8_t* dbg_len;    // [G][1024]
+    uint16_t* codes;     // [G][1024] signed mantissa codes (tail -> pack; 0 where ba == 0)
     const uint8_t* bsf;  // [nblocks] PAC_BS_* flags (block-switching extension), or null: off
 };
 
@@ -612,6 +613,7 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
             // Huffman scoring: lines l = 16 i + q of the 1024, eight at a time (one
             // gather of the ten tables' lengths per line, the loads in flight together)
             const double* ln = K.lines + gl * PAC_HALFN;
+            uint16_t* cs = F.codes + g * PAC_HALFN;
             int acc[PAC_NTAB];
 #pragma unroll
             for (int tb = 0; tb < PAC_NTAB; ++tb) acc[tb] = 0;
@@ -625,10 +627,12 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
                     const int ba = ba_s[r][b];
                     bal[u] = ba;
                     lens[u] = 0;
+                    uint32_t m = 0;
                     if (ba) {
-                        const uint32_t sym = pac_mantissa(ln[l], sf_s[r][b], ba) & ((1u << (ba - 1)) - 1u);
-                        lens[u] = H->lens10[sym];
+                        m = pac_mantissa(ln[l], sf_s[r][b], ba);
+                        lens[u] = H->lens10[m & ((1u << (ba - 1)) - 1u)];
                     }
+                    cs[l] = (uint16_t)m;          // the pack kernel's input
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -680,20 +684,19 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
     return x - v;
 }
 
-// Pass 2: one 256-thread workgroup per stereo block gb (XCD-aware order).
-// The block's MDCT lines are recomputed exactly as k_master_front computes
-// them (same functions, same arithmetic: identical values), then
-// PACFile.WriteDataBlock's packing of both channel-blocks (pacfile.py:288-351):
-// overall(4) tableID(4), per band (ba?ba-1:0)(4) sf(4) [+ nLines sign bits +
-// the Huffman codes], LRMS(25), MSB-first.  Waves 2c and 2c+1 pack channel c,
-// rows 0-7 and 8-15 of its lines; the code-bit prefix crosses the halves
-// through LDS.  A channel-block that would end past cap is skipped; the host
-// reports PAC_E_CAPACITY from the total.
-__global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTables* __restrict__ T,
+// Pass 2: one 256-thread workgroup per block gb (XCD-aware order):
+// PACFile.WriteDataBlock's packing of its channel-blocks (pacfile.py:288-351)
+// from the signed mantissa codes the tail stored (F.codes): overall(4)
+// tableID(4), per band (ba?ba-1:0)(4) sf(4) [+ nLines sign bits + the Huffman
+// codes], LRMS(25) [+ the block-switching bit], MSB-first.  Waves 2c and 2c+1
+// pack channel c, rows 0-7 and 8-15 of its lines; the code-bit prefix crosses
+// the halves through LDS.  A channel-block that would end past cap is
+// skipped; the host reports PAC_E_CAPACITY from the total.
+__global__ __launch_bounds__(256) void k_master_pack(const PacTables* __restrict__ T,
                                                      const PacHuffTables* __restrict__ H, PacMasterFields F,
-                                                     int64_t nblocks, const int64_t* __restrict__ off,
+                                                     int nch, int64_t nblocks, const int64_t* __restrict__ off,
                                                      uint8_t* __restrict__ out, int64_t cap) {
-    __shared__ double2 bufA[1024], bufB[1024];     // 32 KB: MDCT L / R, the coded lines, then the packed words
+    __shared__ uint32_t words[2][PACK_WORDS_MASTER];   // the two channel-blocks' packed bits
     __shared__ int bas[2][PAC_NB], sfs[2][PAC_NB], bstart[2][PAC_NB + 1], pal[2][PAC_NB];
     __shared__ int half_bits[2], tot_bits[2];
     __shared__ uint8_t lr[PAC_NB];
@@ -701,54 +704,23 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
     const int lane = tid & (WAVE - 1);
     const int w = tid / WAVE;
     const int c = w >> 1, h = w & 1;
-    const int nch = src.n_ch;                  // 2, or 1: mono master extension
     const int64_t gb = xcd_item(blockIdx.x, nblocks);
-    const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, nch == 2 ? 1 : 0));
+    const int fl = F.bsf ? F.bsf[gb] : 0;
     if (tid < PAC_NB) lr[tid] = F.lrms[gb * PAC_NB + tid];
     if (tid < nch * PAC_NB) {
         const int cc = tid / PAC_NB, b = tid % PAC_NB;
         bas[cc][b] = F.ba[(gb * nch + cc) * PAC_NB + b];
         sfs[cc][b] = F.sf[(gb * nch + cc) * PAC_NB + b];
     }
-    const int fl = F.bsf ? F.bsf[gb] : 0;     // block-switching flags (pac_bs.h), 0: off
-    const double* XL;
-    const double* XR;
-    if (fl & PAC_BS_SHORT) {                   // as k_master_front: the interleaved short MDCTs
-        double* xl = reinterpret_cast<double*>(bufA);
-        double* xr = reinterpret_cast<double*>(bufB);
-        grp_short_mdct(rL, T, bufA + 512, bufB + 512, xl, tid);
-        if (nch == 2) grp_short_mdct(rR, T, bufA + 512, bufB + 512, xr, tid);
-        XL = xl;
-        XR = nch == 2 ? xr : xl;
-    } else if (fl) {
-        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
-        XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid)
-                      : XL;
-    } else {
-        XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-        XR = nch == 2 ? grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid)
-                      : XL;
-    }
-    const double gL = (double)(1 << F.overall[gb * nch]);
-    const double gR = nch == 2 ? (double)(1 << F.overall[gb * 2 + 1]) : gL;
-    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-    double* L0 = reinterpret_cast<double*>(bufA);
-    double* L1 = reinterpret_cast<double*>(bufB);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {     // each line is read and rewritten by its own thread
-        const int l = i * 256 + tid;
-        const double xl = __dmul_rn(XL[l], gL), xr = __dmul_rn(XR[l], gR);
-        const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
-        const int ms = l < lend ? lr[T->band_of_line[l]] : 0;
-        L0[l] = ms ? M : xl;
-        if (nch == 2) L1[l] = ms ? S : xr;
+    for (int i = tid; i < PACK_WORDS_MASTER; i += 256) {
+        words[0][i] = 0u;
+        words[1][i] = 0u;
     }
     __syncthreads();
     const bool act = c < nch;                  // mono: waves 2, 3 only zero the words and meet the barriers
     const int64_t g = gb * nch + (act ? c : 0);
     const int tb = F.tid[g] - 1;
-    const double* ln = c ? L1 : L0;
+    const uint16_t* cm = F.codes + g * PAC_HALFN;
     // this wave's 8 rows: sign + code of length clen per line (0 for ba == 0 bands)
     uint32_t code[8], sgn[8];
     int clen[8], esc[8], pre[8];
@@ -760,7 +732,7 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
         uint32_t m = 0;
         if (ba && act) {
-            m = pac_mantissa(ln[l], sfs[c][b], ba);
+            m = cm[l];
             const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
             sgn[q] = (m >> (ba - 1)) & 1u;
             const int L = H->len[tb][sym];
@@ -783,12 +755,8 @@ __global__ __launch_bounds__(256) void k_master_pack(PacSource src, const PacTab
         run += t;
     }
     if (act && h == 0 && lane == 0) half_bits[c] = run;
-    __syncthreads();                  // every line read: bufA / bufB become the packed words
-    uint32_t* wd = reinterpret_cast<uint32_t*>(c ? bufB : bufA);
-    for (int i = tid; i < PACK_WORDS_MASTER; i += 256) {
-        reinterpret_cast<uint32_t*>(bufA)[i] = 0u;
-        reinterpret_cast<uint32_t*>(bufB)[i] = 0u;
-    }
+    __syncthreads();
+    uint32_t* wd = words[c];
     if (!act) {
     } else if (h) {
         const int hoff = half_bits[c];

@@ -406,8 +406,12 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         mL = fmax(mL, fabs(xl4[i]));
         mR = fmax(mR, fabs(xr4[i]));
     }
-    atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
-    atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
+    mL = wave_max(mL);                           // one LDS atomic per wave, not per thread
+    mR = wave_max(mR);
+    if ((tid & (WAVE - 1)) == 0) {
+        atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
+        atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
+    }
     __syncthreads();
     const int oL = pac_scale_factor(__longlong_as_double((long long)key[4][0]), 5);
     const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
@@ -448,11 +452,31 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;
         lines[PAC_HALFN + l] = v1;
-        if (l < lend) {
-            atomicMax(&key[0][b], pac_order_key(d0));
-            atomicMax(&key[1][b], pac_order_key(d1));
-            atomicMax(&key[2][b], (unsigned long long)__double_as_longlong(fabs(v0)));
-            atomicMax(&key[3][b], (unsigned long long)__double_as_longlong(fabs(v1)));
+        // band maxima: the wave's 64 consecutive lines hold whole band segments;
+        // a segmented max down to each segment's first lane, then one LDS
+        // atomic per segment (same-address atomics serialise)
+        const bool in = l < lend;
+        const int lane = tid & (WAVE - 1);
+        const int e = in ? min(WAVE - 1, lane + (T->lower[b] + T->nlines[b] - 1 - l)) : lane;
+        unsigned long long k0 = in ? pac_order_key(d0) : 0ull, k1 = in ? pac_order_key(d1) : 0ull;
+        unsigned long long k2 = in ? (unsigned long long)__double_as_longlong(fabs(v0)) : 0ull;
+        unsigned long long k3 = in ? (unsigned long long)__double_as_longlong(fabs(v1)) : 0ull;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const unsigned long long o0 = __shfl_down(k0, off, WAVE), o1 = __shfl_down(k1, off, WAVE);
+            const unsigned long long o2 = __shfl_down(k2, off, WAVE), o3 = __shfl_down(k3, off, WAVE);
+            if (lane + off <= e) {
+                k0 = o0 > k0 ? o0 : k0;
+                k1 = o1 > k1 ? o1 : k1;
+                k2 = o2 > k2 ? o2 : k2;
+                k3 = o3 > k3 ? o3 : k3;
+            }
+        }
+        if (in && (lane == 0 || l == T->lower[b])) {
+            atomicMax(&key[0][b], k0);
+            atomicMax(&key[1][b], k1);
+            atomicMax(&key[2][b], k2);
+            atomicMax(&key[3][b], k3);
         }
     }
     __syncthreads();

@@ -243,6 +243,15 @@ __device__ __forceinline__ double imdct_window_at(const double* U, const PacTabl
     return y * (fl ? bs_long_win(T, fl, n) : T->sine[n]);
 }
 
+// Block switching: wave k turns short block k's lines (Lc[4 j + k]) into
+// U_k = 2 DCT-IV in place; out of line so that the long path keeps its
+// register budget
+__device__ __forceinline__ void dec_short_imdct(double* Lc, const PacTables* __restrict__ T, double2* buf, int tid) {
+    const int k = tid / WAVE;
+    wave_dct4_256([&](int j) { return Lc[4 * j + k]; }, T, buf + 256 * k, tid & (WAVE - 1), 2.0,
+                  [&](int j, double v) { Lc[4 * j + k] = v; });
+}
+
 // Block switching (pac_bs.h): sample p < 2048 of a short frame's synthesis,
 // 0 + the windowed IMDCTs (N = 512) of the short blocks covering p in block
 // order; Uc[4 j + k] = U_k[j] = 2 DCT-IV of block k's lines.
@@ -323,27 +332,14 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
         for (int c = 0; c < nc; ++c) {
             const double* U;
             if (fl & PAC_BS_SHORT) {      // wave k: U_k = 2 DCT-IV of block k, back into its line slots
-                const int k = tid / WAVE;
-                double* Lc = lines[c];
-                wave_dct4_256([&](int j) { return Lc[4 * j + k]; }, T, buf + 256 * k, tid & (WAVE - 1), 2.0,
-                              [&](int j, double v) { Lc[4 * j + k] = v; });
+                dec_short_imdct(lines[c], T, buf, tid);
                 __syncthreads();
-                U = Lc;
+                U = lines[c];
             } else {
                 U = grp_dct4<256>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
             }
             const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
-#pragma unroll
-            for (int i0 = 0; i0 < PAC_HALFN; i0 += 256) {
-                const int i = i0 + tid;
-                double w0, w1;
-                if (fl & PAC_BS_SHORT) {
-                    w0 = short_synth_at(U, T, i);
-                    w1 = short_synth_at(U, T, i + PAC_HALFN);
-                } else {
-                    w0 = imdct_window_at(U, T, i, fl);
-                    w1 = imdct_window_at(U, T, i + PAC_HALFN, fl);
-                }
+            auto emit = [&](int i, double w0, double w1) {
                 if (b >= b0 && b >= 1 - (O.preroll ? 1 : 0)) {
                     const double v = prev[c][i] + w0;
                     const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
@@ -351,6 +347,21 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
                     if (O.fpcm) O.fpcm[o] = v;
                 }
                 prev[c][i] = w1;
+            };
+            if (fl & PAC_BS_SHORT) {
+#pragma unroll 1
+                for (int i = tid; i < PAC_HALFN; i += 256)
+                    emit(i, short_synth_at(U, T, i), short_synth_at(U, T, i + PAC_HALFN));
+            } else if (fl) {               // start / stop window
+#pragma unroll 1
+                for (int i = tid; i < PAC_HALFN; i += 256)
+                    emit(i, imdct_window_at(U, T, i, fl), imdct_window_at(U, T, i + PAC_HALFN, fl));
+            } else {
+#pragma unroll
+                for (int i0 = 0; i0 < PAC_HALFN; i0 += 256) {
+                    const int i = i0 + tid;
+                    emit(i, imdct_window_at(U, T, i, 0), imdct_window_at(U, T, i + PAC_HALFN, 0));
+                }
             }
             __syncthreads();      // U (buf) is rewritten by the next channel / block
         }

@@ -169,7 +169,6 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
                                                            PacOriginWork W, int64_t G) {
     __shared__ double2 buf[1024];          // 16 KB: MDCT scratch / spectrum / masker list / SMR
     __shared__ __attribute__((aligned(16))) double xs[PAC_N];   // 16 KB: sine-windowed block, then the loud masker list
-    __shared__ int16_t rank[PAC_HALFN];   // 2 KB: masker rank of each bin (4 workgroups per CU)
     // the small reduction scratch lives in whichever region is idle at that point
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -214,7 +213,7 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
     grp_spectrum_pow<FRONT_NT>([&](int i) { return __dmul_rn(xs[i], T->hann[i]); }, T, buf,
                                reinterpret_cast<double2*>(xs), tid);
     PROF_MARK(4);
-    const MaskerLists L = masker_lists(buf, xs, rank);
+    const MaskerLists L = masker_lists(buf, xs);
     int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, L);
     PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
@@ -502,11 +501,10 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
                                                         int32_t* __restrict__ npeaks) {
     __shared__ double2 buf[1024];
     __shared__ double2 tmp[1024];
-    __shared__ int16_t rank[PAC_HALFN];
     const int lane = threadIdx.x;
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
     wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
-    const MaskerLists L = masker_lists(buf, tmp, rank);
+    const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<WAVE>(buf, T, no_drop ? 0.0 : 15.0, lane, L);
 #pragma unroll 1
     for (int q = 0; q < 16; ++q)

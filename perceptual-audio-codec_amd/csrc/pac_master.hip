@@ -96,7 +96,6 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
                                                          PacMasterChunk ck) {
     __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
     __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // FFT scratch, then loud list (region B)
-    __shared__ int16_t rank[PAC_HALFN];
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
@@ -110,7 +109,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
     // the M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
     // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
-    __shared__ int rowmask;
+    int& rowmask = reinterpret_cast<int*>(tmp)[0];          // region B is idle until the spectrum
     if (tid == 0) rowmask = 0;
     __syncthreads();
     {
@@ -132,7 +131,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
-    const MaskerLists L = masker_lists(buf, tmp, rank);
+    const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     // rows claimed dynamically, most expensive first (as in k_origin_front)

@@ -352,19 +352,21 @@ __device__ __forceinline__ void dd_add(double ah, double al, double bh, double b
 //   pfh/pfl  exclusive dd prefix of E_m            (flat zone)
 //   sl       suffix sum from m of 2^(B + KL(z - 1/2))   (lower side; sl[nm] = 0)
 //   su       exclusive prefix of 2^(B - KL(z + 1/2)) over quiet maskers (upper side)
-// Region B (16 KB, the FFT scratch): the loud maskers' z, B, ku (12 KB), lpre
-// [m] = #loud maskers of rank < m, a few counters and the peak-compaction
-// scratch.  rank[k] (k < 1024) = #maskers with bin < k.
+// Region B (16 KB, the FFT scratch): the loud maskers' z, B, ku (12 KB; the
+// peak-compaction scratch kidx lives in their first 2 KB until they are
+// written), lpre[m] = #loud maskers of rank < m, a few counters, and
+// rank[k] (k < 1024) = #maskers with bin < k -- so a threshold workgroup
+// needs exactly the two 16 KB regions (5 workgroups per CU).
 struct MaskerLists {
     double *pfh, *pfl, *sl, *su;
     double *lz, *lB, *lku;
     int16_t* lpre;
     int* misc;       // [0] row counter of the claiming loop, [1] loud count
     int* cnt;        // 32 ints: ballot segment counts
-    int* kidx;       // 512 ints: compacted peak bins
+    int* kidx;       // 512 ints: compacted peak bins (aliases lz: dead before lz is written)
     int16_t* rank;
 };
-__device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB, int16_t* rank) {
+__device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB) {
     MaskerLists L;
     double* a = reinterpret_cast<double*>(regA);
     L.pfh = a;
@@ -378,8 +380,8 @@ __device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB, int1
     L.lpre = reinterpret_cast<int16_t*>(b + 12288);
     L.misc = reinterpret_cast<int*>(b + 13312);
     L.cnt = reinterpret_cast<int*>(b + 13312 + 64);
-    L.kidx = reinterpret_cast<int*>(b + 14336);
-    L.rank = rank;
+    L.kidx = reinterpret_cast<int*>(b);
+    L.rank = reinterpret_cast<int16_t*>(b + 14336);
     return L;
 }
 

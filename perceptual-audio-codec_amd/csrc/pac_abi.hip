@@ -320,7 +320,11 @@ struct pac_ctx {
     DevBuf<uint8_t> dec_bsf;                // decoder: the short-frame bit per channel-block
     hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
     hipStream_t stream3 = nullptr;          // master: the LRMS decisions, running ahead of the thresholds
-    bool lrms_async = true;                 // PAC_LRMS_ASYNC=0: LRMS in line on the front stream
+    // PAC_LRMS_ASYNC=1: LRMS on its own stream, running ahead of the thresholds.
+    // Off by default: since k_master_lrms fits 5 workgroups per CU the overlap
+    // no longer gains (3.71 vs 3.72 M blocks/s) and in line every kernel's
+    // event time is its own (clean per-kernel rooflines)
+    bool lrms_async = false;
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
     DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)

@@ -282,23 +282,26 @@ __device__ double2 np_csum_combine(const double2* leaf, int& idx, int n) {
     return make_double2(a.x + b.x, a.y + b.y);
 }
 
-// complex spectrum X[k], k < 1024, of a real 2048-block d: staged in buf,
-// Stockham FFT into tmp, real split back into buf
+// complex spectrum X[k], k < 1024, of a real 2048-block d, all in buf: the
+// sample pairs staged, the one-buffer Stockham FFT, the real split in place
+// (thread p reads and writes its own bin pair p, 1024 - p)
 template <int NT, class DS>
 __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* __restrict__ T, double2* buf,
-                                                  double2* tmp, int tid) {
+                                                  int tid) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
         const int n = n0 + tid;
         buf[n] = make_double2(d(2 * n), d(2 * n + 1));
     }
-    const double2* Z = grp_fft_stockham<10, NT>(buf, tmp, T->fft_tw, tid);   // = tmp
+    grp_fft_stockham_1buf<10, NT>(buf, T->fft_tw, tid);
+    const double2* Z = buf;
 #pragma unroll
     for (int p0 = 0; p0 < 512; p0 += NT) {
         const int p = p0 + tid;
         int kk[2];
         kk[0] = p;
         kk[1] = p ? 1024 - p : 512;
+        double2 X[2];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             const double2 A = Z[kk[side]];
@@ -306,8 +309,10 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
             const double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
             const double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
             const double2 wo = cmul(T->rfft_tw[kk[side]], o);
-            buf[kk[side]] = make_double2(e.x + wo.y, e.y - wo.x);
+            X[side] = make_double2(e.x + wo.y, e.y - wo.x);
         }
+        buf[kk[0]] = X[0];
+        buf[kk[1]] = X[1];
     }
     grp_sync<NT>();
 }
@@ -318,20 +323,20 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 // that k_master_thr computes only the thresholds a band's coding mode uses.
 __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTables* __restrict__ T,
                                                      PacMasterFields F, PacMasterChunk ck) {
-    __shared__ double2 bufA[1024], bufB[1024], bufC[1024];    // 48 KB
-    __shared__ double2 leafv[2][64];
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
-    grp_spectrum_cplx<256>([&](int i) { return rL(i); }, T, bufA, bufC, tid);
-    grp_spectrum_cplx<256>([&](int i) { return rR(i); }, T, bufB, bufC, tid);
+    grp_spectrum_cplx<256>([&](int i) { return rL(i); }, T, bufA, tid);
+    grp_spectrum_cplx<256>([&](int i) { return rR(i); }, T, bufB, tid);
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
     };
+    double2 lv0 = make_double2(0.0, 0.0), lv1 = lv0;
     if (tid < T->lr_nleaf) {
         const int b = T->lr_leaf_band[tid], e0 = T->lr_leaf_e0[tid], n = T->lr_leaf_n[tid];
         const int lo = T->lower[b];
@@ -343,15 +348,19 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
             const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
             return make_double2(__dadd_rn(a.x, c.x), __dadd_rn(a.y, c.y));
         };
-        leafv[0][tid] = np_csum_leaf(fd, e0, n);
-        leafv[1][tid] = np_csum_leaf(fs, e0, n);
+        lv0 = np_csum_leaf(fd, e0, n);
+        lv1 = np_csum_leaf(fs, e0, n);
     }
+    __syncthreads();                               // every spectrum read: bufA's start holds the leaves
+    double2* leafv0 = bufA;
+    double2* leafv1 = bufA + 64;
+    if (tid < 64) { leafv0[tid] = lv0; leafv1[tid] = lv1; }
     __syncthreads();
     if (tid < PAC_NB) {
         int i0 = T->lr_first_leaf[tid], i1 = i0;
         const int n = 2 * T->nlines[tid];
-        const double2 sd = np_csum_combine<5>(leafv[0], i0, n);
-        const double2 ss = np_csum_combine<5>(leafv[1], i1, n);
+        const double2 sd = np_csum_combine<5>(leafv0, i0, n);
+        const double2 ss = np_csum_combine<5>(leafv1, i1, n);
         F.lrms[gb * PAC_NB + tid] = (uint8_t)(hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0);
     }
 }

@@ -179,6 +179,77 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
     return src;
 }
 
+// The same Stockham FFT in ONE buffer: each stage reads its four inputs into
+// registers, waits until every thread has read, then writes its outputs in
+// place of them -- identical arithmetic (bit-identical results) with half the
+// LDS.  Result in buf.
+template <int LOG, int NT>
+__device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double2* __restrict__ tw, int tid) {
+    constexpr int N = 1 << LOG;
+    constexpr int N4 = N / 4;
+    constexpr int J = N4 >= NT ? N4 / NT : 1;
+    static_assert(N4 % NT == 0 || N4 < NT, "stage items per thread");
+#pragma unroll
+    for (int st = 0; st < LOG / 2; ++st) {
+        const int Ns = 1 << (2 * st);
+        double2 v[J][4];
+        grp_sync<NT>();
+#pragma unroll
+        for (int q = 0; q < J; ++q) {
+            const int j = q * NT + tid;
+            if (N4 < NT && j >= N4) break;
+            const int k = j & (Ns - 1);
+            v[q][0] = buf[j];
+            v[q][1] = buf[j + N4];
+            v[q][2] = buf[j + 2 * N4];
+            v[q][3] = buf[j + 3 * N4];
+            if (Ns > 1) {
+                const int e = k * (256 / Ns);
+                v[q][1] = cmul(v[q][1], tw[e]);
+                v[q][2] = cmul(v[q][2], tw[2 * e]);
+                v[q][3] = cmul(v[q][3], tw[3 * e]);
+            }
+        }
+        grp_sync<NT>();
+#pragma unroll
+        for (int q = 0; q < J; ++q) {
+            const int j = q * NT + tid;
+            if (N4 < NT && j >= N4) break;
+            const int k = j & (Ns - 1);
+            const double2 a0 = make_double2(v[q][0].x + v[q][2].x, v[q][0].y + v[q][2].y);
+            const double2 a1 = make_double2(v[q][0].x - v[q][2].x, v[q][0].y - v[q][2].y);
+            const double2 a2 = make_double2(v[q][1].x + v[q][3].x, v[q][1].y + v[q][3].y);
+            const double2 a3 = make_double2(v[q][1].y - v[q][3].y, v[q][3].x - v[q][1].x);
+            const int o = ((j - k) << 2) + k;
+            buf[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
+            buf[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
+            buf[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
+            buf[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+        }
+    }
+    if (LOG & 1) {
+        constexpr int J2 = (N / 2) >= NT ? (N / 2) / NT : 1;
+        double2 v0[J2], v1[J2];
+        grp_sync<NT>();
+#pragma unroll
+        for (int q = 0; q < J2; ++q) {
+            const int j = q * NT + tid;
+            if ((N / 2) < NT && j >= N / 2) break;
+            v0[q] = buf[j];
+            v1[q] = cmul(buf[j + N / 2], tw[j * (1024 / N)]);
+        }
+        grp_sync<NT>();
+#pragma unroll
+        for (int q = 0; q < J2; ++q) {
+            const int j = q * NT + tid;
+            if ((N / 2) < NT && j >= N / 2) break;
+            buf[j] = make_double2(v0[q].x + v1[q].x, v0[q].y + v1[q].y);
+            buf[j + N / 2] = make_double2(v0[q].x - v1[q].x, v0[q].y - v1[q].y);
+        }
+    }
+    grp_sync<NT>();
+}
+
 // DCT-IV of 1024 values v(j), scaled by sc (a power of two):
 //   X[k] = sc * sum_j v(j) cos(pi/1024 (j + 1/2)(k + 1/2)),
 // via the 512-point complex Stockham FFT (even/odd interleave, pre- and

@@ -372,9 +372,11 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
 __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
                                                       PacMasterChunkBuf K, PacMasterFields F,
                                                       PacMasterChunk ck) {
-    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
-    __shared__ uint8_t lrms_s[PAC_NB];
-    __shared__ unsigned long long key[6][32];    // SMR 0/1, |line| 0/1, max|X| L/R
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB (5 workgroups per CU)
+    // after the MDCTs: SMR 0/1, |line| 0/1, max|X| L/R keys and the LRMS flags
+    // in the free upper half of bufB
+    unsigned long long (*key)[32] = reinterpret_cast<unsigned long long (*)[32]>(bufB + 512);
+    uint8_t* lrms_s = reinterpret_cast<uint8_t*>(bufB + 640);
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     int64_t gb;
@@ -384,9 +386,6 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     const bool sh = fl & PAC_BS_SHORT;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, st ? 1 : 0));
-    if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
-    if (tid < PAC_NB) lrms_s[tid] = F.lrms[gb * PAC_NB + tid];
-    __syncthreads();
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
     const double* XL;
@@ -405,6 +404,10 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
         if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
     }
+    // (every MDCT ended with a barrier: the upper halves are free)
+    if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
+    if (tid < PAC_NB) lrms_s[tid] = F.lrms[gb * PAC_NB + tid];
+    __syncthreads();
     double xl4[4], xr4[4];
     double mL = 0.0, mR = 0.0;
 #pragma unroll

@@ -89,7 +89,7 @@ __device__ __forceinline__ void grp_short_mdct(const XR& x, const PacTables* __r
 // |FFT(d)[k]|^2, k < 256, of a real 512-sample short block d(i) by one wave:
 // 256-point complex Stockham FFT of the sample pairs + the real split
 // (twiddles exp(-2 pi i k / 512) = rfft_tw[4 k]).  buf, tmp: 256 double2 each;
-// on return pw[k] (may alias neither) holds the powers.
+// on return pw[k] holds the powers (pw may alias tmp: the FFT ends in buf).
 template <class DS>
 __device__ __forceinline__ void wave_spectrum_pow_short(const DS& d, const PacTables* __restrict__ T, double2* buf,
                                                         double2* tmp, double* pw, int lane) {

@@ -158,11 +158,15 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
 __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const PacTables* __restrict__ T,
                                                           PacMasterChunkBuf K, PacMasterFields F,
                                                           PacMasterChunk ck) {
-    __shared__ double2 bufs[4][2][256];                     // per wave: FFT buffer + scratch (32 KB)
-    __shared__ double pw[4][256];
-    __shared__ double mz[4][128], mS[4][128], mlev[4][128];
-    __shared__ int kidx[4][128];
+    // per wave (8 KB): FFT buffer + scratch; then the powers in the scratch and
+    // the masker list in the FFT buffer
+    __shared__ double2 bufs[4][2][256];
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), k = tid / WAVE;
+    double* pw = reinterpret_cast<double*>(bufs[k][1]);
+    double* mz = reinterpret_cast<double*>(bufs[k][0]);
+    double* mS = mz + 128;
+    double* mlev = mz + 256;
+    int* kidx = reinterpret_cast<int*>(mz + 384);
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
     const int nvar = ck.nch == 2 ? 6 : 1;
     const int64_t j = item / nvar;
@@ -184,9 +188,9 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
         if (v >= 4) ms = __dmul_rn(ms, h);
         return ms;
     };
-    wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw[k], lane);
+    wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw, lane);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
-    wave_threshold_short(pw[k], T, v >= 4 ? 0.0 : 15.0, mz[k], mS[k], mlev[k], kidx[k], lane,
+    wave_threshold_short(pw, T, v >= 4 ? 0.0 : 15.0, mz, mS, mlev, kidx, lane,
                          [&](int l, double t) { out[4 * l + k] = t; });
 }
 

@@ -456,6 +456,7 @@ PHASES = {  # pac_timing field -> kernel, per profile (include/pac_gpu.h)
                ("alloc_ms", "k_master_tail"),
                ("pack_ms", "k_master_pack"), ("scan_ms", "k_scan")],
 }
+PHASES["bs"] = PHASES["master"] + [("thr_short_ms", "k_master_thr_short")]
 
 
 def main():
@@ -476,7 +477,7 @@ def main():
         return
 
     def step():
-        ms = {f: 0.0 for f, _ in PHASES[a.profile]}
+        ms = {f: 0.0 for f, _ in PHASES["bs" if a.bs else a.profile]}
         for j in jobs:
             t = j.run()
             for f in ms:
@@ -500,7 +501,7 @@ def main():
     total_blocks = dist.sum(blocks)
     value = total_blocks / (el_max / a.steps)
 
-    kern_ms = {k: float(np.mean([p[f] for p in per])) for f, k in PHASES[a.profile]}
+    kern_ms = {k: float(np.mean([p[f] for p in per])) for f, k in PHASES["bs" if a.bs else a.profile]}
     # the dominant kernel on the critical path (the master reservoir tail runs on
     # a second stream, overlapped with the next chunk's thresholds)
     dom = max((k for k in kern_ms if k != "k_master_tail"), key=kern_ms.get)

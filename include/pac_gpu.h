@@ -96,11 +96,12 @@ typedef struct {
     float alloc_ms;
     float scan_ms;
     float pack_ms;
-    float total_ms;     /* origin: first to last event; master: lrms+thr+front+scan+pack */
+    float total_ms;     /* origin: first to last event; master: lrms+thr(+thr_short)+front+scan+pack */
     int64_t n_channel_blocks;
     int64_t out_bytes;
     float thr_ms;
     float lrms_ms;
+    float thr_short_ms; /* block switching: k_master_thr_short (the short frames' thresholds) */
 } pac_timing;
 
 /* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */

@@ -714,6 +714,7 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     if (!c->timing) return;
     c->last.thr_ms = 0.f;
     c->last.lrms_ms = 0.f;
+    c->last.thr_short_ms = 0.f;
     hipEventSynchronize(c->ev[4]);
     hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
     hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
@@ -834,10 +835,12 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                 if ((rc = mark(0, 5))) return rc;
             }
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
-            if (F.bsf)     // the short frames' thresholds (the long kernel skips them)
+            if ((rc = mark(0, 0))) return rc;
+            if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
                 hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(B * nvar)), dim3(256), 0, s0, src, T, K, F,
                                    ck);
-            if ((rc = mark(0, 0))) return rc;
+                if ((rc = mark(0, 6))) return rc;
+            }
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             HIPCHK(hipGetLastError());
             if ((rc = mark(0, 1))) return rc;
@@ -870,7 +873,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s0));
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
-        float ph[6] = {0, 0, 0, 0, 0, 0};
+        float ph[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < 3; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
@@ -884,7 +887,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         c->last.pack_ms = ph[3];
         c->last.scan_ms = ph[4];
         c->last.lrms_ms = ph[5];
-        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5];   // the tail overlaps the next chunk
+        c->last.thr_short_ms = ph[6];
+        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5] + ph[6];   // the tail overlaps the next chunk
         c->last.n_channel_blocks = G;
         c->last.out_bytes = 0;
     }

@@ -340,25 +340,55 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
     };
+    // leaf sums (np_csum_leaf) of both sums -- sum(L^2 - R^2) and sum(L^2 + R^2) --
+    // by the four lanes of a quad per leaf: lane `sub` runs numpy's accumulators
+    // r[2 sub], r[2 sub + 1] (complex elements e0 + 4 k + sub) in order, the
+    // quad then combines ((r0 + r2) + (r4 + r6)) by DPP, lane 0 adds the tail
+    // elements: numpy's exact operation order
+    const int lf = tid >> 2, sub = tid & 3;
+    const bool has = lf < T->lr_nleaf;
+    int e0 = 0, n = 0, lo = 0;
+    if (has) {
+        e0 = T->lr_leaf_e0[lf];
+        n = T->lr_leaf_n[lf];
+        lo = T->lower[T->lr_leaf_band[lf]];
+    }
+    auto zz = [&](int e, double2& d, double2& sm) {
+        const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
+        d = make_double2(__dsub_rn(a.x, c.x), __dsub_rn(a.y, c.y));
+        sm = make_double2(__dadd_rn(a.x, c.x), __dadd_rn(a.y, c.y));
+    };
+    const int nfull = n >= 8 ? n - n % 8 : 0;
+    double2 rd = make_double2(0.0, 0.0), rs = rd;
+    for (int i = 0; i < nfull; i += 8) {
+        double2 d, sm;
+        zz(e0 + i / 2 + sub, d, sm);
+        if (i == 0) { rd = d; rs = sm; }
+        else {
+            rd.x = __dadd_rn(rd.x, d.x); rd.y = __dadd_rn(rd.y, d.y);
+            rs.x = __dadd_rn(rs.x, sm.x); rs.y = __dadd_rn(rs.y, sm.y);
+        }
+    }
+    auto quad2 = [](double v) {
+        const double a = v + dpp_full_f64<PAC_DPP_QXOR1>(v);      // r[2s] + r[2s+2] pairs
+        return a + dpp_full_f64<PAC_DPP_QXOR2>(a);
+    };
+    rd.x = quad2(rd.x); rd.y = quad2(rd.y);
+    rs.x = quad2(rs.x); rs.y = quad2(rs.y);
     double2 lv0 = make_double2(0.0, 0.0), lv1 = lv0;
-    if (tid < T->lr_nleaf) {
-        const int b = T->lr_leaf_band[tid], e0 = T->lr_leaf_e0[tid], n = T->lr_leaf_n[tid];
-        const int lo = T->lower[b];
-        auto fd = [&](int e) {
-            const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
-            return make_double2(__dsub_rn(a.x, c.x), __dsub_rn(a.y, c.y));
-        };
-        auto fs = [&](int e) {
-            const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
-            return make_double2(__dadd_rn(a.x, c.x), __dadd_rn(a.y, c.y));
-        };
-        lv0 = np_csum_leaf(fd, e0, n);
-        lv1 = np_csum_leaf(fs, e0, n);
+    if (has && sub == 0) {
+        if (n >= 8) { lv0 = rd; lv1 = rs; }
+        for (int i = nfull; i < n; i += 2) {      // the tail (n < 8: the whole plain loop from 0)
+            double2 d, sm;
+            zz(e0 + i / 2, d, sm);
+            lv0.x = __dadd_rn(lv0.x, d.x); lv0.y = __dadd_rn(lv0.y, d.y);
+            lv1.x = __dadd_rn(lv1.x, sm.x); lv1.y = __dadd_rn(lv1.y, sm.y);
+        }
     }
     __syncthreads();                               // every spectrum read: bufA's start holds the leaves
     double2* leafv0 = bufA;
     double2* leafv1 = bufA + 64;
-    if (tid < 64) { leafv0[tid] = lv0; leafv1[tid] = lv1; }
+    if (has && sub == 0) { leafv0[lf] = lv0; leafv1[lf] = lv1; }
     __syncthreads();
     if (tid < PAC_NB) {
         int i0 = T->lr_first_leaf[tid], i1 = i0;

@@ -321,6 +321,44 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
     grp_sync<NT>();
 }
 
+// the complex spectra of two real 2048-blocks dA, dB at once (as
+// grp_spectrum_cplx on each: bit-identical), both FFTs stage by stage together
+template <int NT, class DA, class DB>
+__device__ __forceinline__ void grp_spectrum_cplx2(const DA& dA, const DB& dB, const PacTables* __restrict__ T,
+                                                   double2* bufA, double2* bufB, int tid) {
+#pragma unroll 4
+    for (int n0 = 0; n0 < 1024; n0 += NT) {
+        const int n = n0 + tid;
+        bufA[n] = make_double2(dA(2 * n), dA(2 * n + 1));
+        bufB[n] = make_double2(dB(2 * n), dB(2 * n + 1));
+    }
+    grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid);
+#pragma unroll
+    for (int p0 = 0; p0 < 512; p0 += NT) {
+        const int p = p0 + tid;
+        int kk[2];
+        kk[0] = p;
+        kk[1] = p ? 1024 - p : 512;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            double2* Z = u ? bufB : bufA;
+            double2 X[2];
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const double2 A = Z[kk[side]];
+                const double2 Bc = Z[(1024 - kk[side]) & 1023];
+                const double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
+                const double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
+                const double2 wo = cmul(T->rfft_tw[kk[side]], o);
+                X[side] = make_double2(e.x + wo.y, e.y - wo.x);
+            }
+            Z[kk[0]] = X[0];
+            Z[kk[1]] = X[1];
+        }
+    }
+    grp_sync<NT>();
+}
+
 // One 256-thread workgroup per stereo block: the LRMS decision (codec.py:94-102)
 // |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band, over the complex FFT bins
 // of the raw (unwindowed) blocks, with numpy's pairwise sums.  It runs first so
@@ -334,8 +372,7 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, 1));
-    grp_spectrum_cplx<256>([&](int i) { return rL(i); }, T, bufA, tid);
-    grp_spectrum_cplx<256>([&](int i) { return rR(i); }, T, bufB, tid);
+    grp_spectrum_cplx2<256>([&](int i) { return rL(i); }, [&](int i) { return rR(i); }, T, bufA, bufB, tid);
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));

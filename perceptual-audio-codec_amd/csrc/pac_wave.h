@@ -250,6 +250,61 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
     grp_sync<NT>();
 }
 
+// Two independent one-buffer Stockham FFTs (buffers a and b) advanced stage by
+// stage together: each thread's butterflies of both in flight, one pair of
+// barriers per stage for both.  Bit-identical to grp_fft_stockham_1buf on each.
+template <int LOG, int NT>
+__device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b, const double2* __restrict__ tw,
+                                                         int tid) {
+    constexpr int N = 1 << LOG;
+    constexpr int N4 = N / 4;
+    static_assert(N4 % NT == 0 && !(LOG & 1), "one radix-4 butterfly set per thread and stage");
+    constexpr int J = N4 / NT;
+    double2* bufs[2] = {a, b};
+#pragma unroll
+    for (int st = 0; st < LOG / 2; ++st) {
+        const int Ns = 1 << (2 * st);
+        double2 v[2][J][4];
+        grp_sync<NT>();
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int q = 0; q < J; ++q) {
+                const int j = q * NT + tid;
+                const int k = j & (Ns - 1);
+                v[u][q][0] = bufs[u][j];
+                v[u][q][1] = bufs[u][j + N4];
+                v[u][q][2] = bufs[u][j + 2 * N4];
+                v[u][q][3] = bufs[u][j + 3 * N4];
+                if (Ns > 1) {
+                    const int e = k * (256 / Ns);
+                    v[u][q][1] = cmul(v[u][q][1], tw[e]);
+                    v[u][q][2] = cmul(v[u][q][2], tw[2 * e]);
+                    v[u][q][3] = cmul(v[u][q][3], tw[3 * e]);
+                }
+            }
+        grp_sync<NT>();
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int q = 0; q < J; ++q) {
+                const int j = q * NT + tid;
+                const int k = j & (Ns - 1);
+                const double2* w = v[u][q];
+                const double2 a0 = make_double2(w[0].x + w[2].x, w[0].y + w[2].y);
+                const double2 a1 = make_double2(w[0].x - w[2].x, w[0].y - w[2].y);
+                const double2 a2 = make_double2(w[1].x + w[3].x, w[1].y + w[3].y);
+                const double2 a3 = make_double2(w[1].y - w[3].y, w[3].x - w[1].x);
+                const int o = ((j - k) << 2) + k;
+                bufs[u][o] = make_double2(a0.x + a2.x, a0.y + a2.y);
+                bufs[u][o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
+                bufs[u][o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
+                bufs[u][o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+            }
+    }
+    grp_sync<NT>();
+}
+
 // DCT-IV of 1024 values v(j), scaled by sc (a power of two):
 //   X[k] = sc * sum_j v(j) cos(pi/1024 (j + 1/2)(k + 1/2)),
 // via the 512-point complex Stockham FFT (even/odd interleave, pre- and

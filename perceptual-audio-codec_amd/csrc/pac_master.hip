@@ -471,9 +471,13 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     } else if (fl) {   // long frame next to a short one: start / stop window
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
         if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid);
+    } else if (st) {   // both channels' MDCTs stage by stage together
+        grp_mdct2<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); },
+                       [&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufA, bufB, tid);
+        XL = reinterpret_cast<const double*>(bufA);
+        XR = reinterpret_cast<const double*>(bufB);
     } else {
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
-        if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufB, tid);
     }
     // (every MDCT ended with a barrier: the upper halves are free)
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;

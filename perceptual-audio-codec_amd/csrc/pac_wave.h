@@ -305,6 +305,74 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
     grp_sync<NT>();
 }
 
+// Two independent ping-pong Stockham FFTs (src/dst pairs a, b) advanced stage
+// by stage together: one barrier per stage for both, bit-identical to
+// grp_fft_stockham on each.  Returns the result buffer of a (the one of b is
+// the matching buffer of its pair).
+template <int LOG, int NT>
+__device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, double2* sb, double2* db,
+                                                    const double2* __restrict__ tw, int tid,
+                                                    double2** ra, double2** rb) {
+    constexpr int N = 1 << LOG;
+    constexpr int N4 = N / 4;
+#pragma unroll
+    for (int st = 0; st < LOG / 2; ++st) {
+        const int Ns = 1 << (2 * st);
+        grp_sync<NT>();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const double2* src = u ? sb : sa;
+            double2* dst = u ? db : da;
+#pragma unroll
+            for (int j0 = 0; j0 < N4; j0 += NT) {
+                const int j = j0 + tid;
+                if (N4 % NT != 0 && j >= N4) break;
+                const int k = j & (Ns - 1);
+                double2 v0 = src[j], v1 = src[j + N4], v2 = src[j + 2 * N4], v3 = src[j + 3 * N4];
+                if (Ns > 1) {
+                    const int e = k * (256 / Ns);
+                    v1 = cmul(v1, tw[e]);
+                    v2 = cmul(v2, tw[2 * e]);
+                    v3 = cmul(v3, tw[3 * e]);
+                }
+                const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
+                const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
+                const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
+                const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);
+                const int o = ((j - k) << 2) + k;
+                dst[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
+                dst[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
+                dst[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
+                dst[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+            }
+        }
+        double2* t = sa; sa = da; da = t;
+        t = sb; sb = db; db = t;
+    }
+    if (LOG & 1) {
+        grp_sync<NT>();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const double2* src = u ? sb : sa;
+            double2* dst = u ? db : da;
+#pragma unroll
+            for (int j0 = 0; j0 < N / 2; j0 += NT) {
+                const int j = j0 + tid;
+                if ((N / 2) % NT != 0 && j >= N / 2) break;
+                const double2 v0 = src[j];
+                const double2 v1 = cmul(src[j + N / 2], tw[j * (1024 / N)]);
+                dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
+                dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
+            }
+        }
+        double2* t = sa; sa = da; da = t;
+        t = sb; sb = db; db = t;
+    }
+    grp_sync<NT>();
+    *ra = sa;
+    *rb = sb;
+}
+
 // DCT-IV of 1024 values v(j), scaled by sc (a power of two):
 //   X[k] = sc * sum_j v(j) cos(pi/1024 (j + 1/2)(k + 1/2)),
 // via the 512-point complex Stockham FFT (even/odd interleave, pre- and
@@ -351,6 +419,46 @@ __device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __res
     }
     grp_sync<NT>();
     return X;
+}
+
+// Two MDCTs at once (grp_mdct of xa into bufA and of xb into bufB, FFTs
+// stage by stage together): bit-identical to two grp_mdct calls.
+template <int NT, class FA, class FB>
+__device__ __forceinline__ void grp_mdct2(const FA& xa, const FB& xb, const PacTables* __restrict__ T,
+                                          double2* bufA, double2* bufB, int tid) {
+    auto folda = [&](int n) {
+        return n < 512 ? __dsub_rn(-xa(1535 - n), xa(1536 + n)) : __dsub_rn(xa(n - 512), xa(1535 - n));
+    };
+    auto foldb = [&](int n) {
+        return n < 512 ? __dsub_rn(-xb(1535 - n), xb(1536 + n)) : __dsub_rn(xb(n - 512), xb(1535 - n));
+    };
+#pragma unroll
+    for (int q0 = 0; q0 < 512; q0 += NT) {
+        const int q = q0 + tid;
+        bufA[q] = cmul(make_double2(folda(2 * q), folda(1023 - 2 * q)), T->mdct_pre[q]);
+        bufB[q] = cmul(make_double2(foldb(2 * q), foldb(1023 - 2 * q)), T->mdct_pre[q]);
+    }
+    double2 *Ya, *Yb;
+    grp_fft_stockham_x2<9, NT>(bufA, bufA + 512, bufB, bufB + 512, T->fft_tw, tid, &Ya, &Yb);   // = buf + 512
+    double* XA = reinterpret_cast<double*>(bufA);
+    double* XB = reinterpret_cast<double*>(bufB);
+#pragma unroll
+    for (int q0 = 0; q0 < 512; q0 += NT) {
+        const int q = q0 + tid;
+        const double2 ya = cmul(Ya[q], T->mdct_post[q]), yb = cmul(Yb[q], T->mdct_post[q]);
+        XA[2 * q] = ya.x * (1.0 / 1024.0);
+        XA[1023 - 2 * q] = -ya.y * (1.0 / 1024.0);
+        XB[2 * q] = yb.x * (1.0 / 1024.0);
+        XB[1023 - 2 * q] = -yb.y * (1.0 / 1024.0);
+    }
+    grp_sync<NT>();
+#pragma unroll
+    for (int k0 = 0; k0 < 1024; k0 += NT) {
+        const int k = k0 + tid;
+        if (XA[k] == 0.0) XA[k] = T->mdct_zero_neg[k] ? -0.0 : 0.0;
+        if (XB[k] == 0.0) XB[k] = T->mdct_zero_neg[k] ? -0.0 : 0.0;
+    }
+    grp_sync<NT>();
 }
 
 // |FFT(d)[k]|^2, k < 1024, of a real 2048-sample block d(i) via a 1024-point

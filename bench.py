@@ -100,7 +100,16 @@ class Dist:
         self.td = None
         if self.world > 1:
             import torch.distributed as td
-            td.init_process_group("gloo")
+            # gloo's connection banner goes to fd 1: keep stdout for the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                td.init_process_group("gloo")
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.td = td
 
     def barrier(self):
@@ -462,7 +471,10 @@ PHASES["bs"] = PHASES["master"] + [("thr_short_ms", "k_master_thr_short")]
 def main():
     a = parse()
     dist = Dist()
-    ctx = _lib.Context(dist.local, huffman=a.master)
+    # one GPU per rank (LOCAL_RANK); PAC_BENCH_SHARE_GPU=1 puts every rank on
+    # device 0 -- a rehearsal of the multi-rank path on a one-GPU box only
+    dev = 0 if os.environ.get("PAC_BENCH_SHARE_GPU") == "1" else dist.local
+    ctx = _lib.Context(dev, huffman=a.master)
     desc, stereo = None, None
     if a.config == 3:
         jobs, desc, stereo = file_jobs(a, ctx, dist.rank, dist.world)

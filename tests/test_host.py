@@ -264,3 +264,32 @@ def test_decode_layout_on_host(name, prof):
     so2 = np.array([0, len(data) - 3], dtype=np.int64)
     assert L.pac_decode_layout(C.byref(p), 1, data.ctypes.data, so2.ctypes.data_as(P64), 0,
                                fo.ctypes.data_as(P64)) == -1
+
+
+BENCH_DIST_WORKER = r"""
+import importlib.util, sys
+sys.argv = ["bench.py"]
+spec = importlib.util.spec_from_file_location("bench", "%s/bench.py")
+b = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(b)
+d = b.Dist()
+d.barrier()
+if d.rank == 0:
+    print("MAX %%s SUM %%s" %% (d.max(d.rank + 1.5), d.sum(d.rank + 1)))
+else:
+    d.max(d.rank + 1.5), d.sum(d.rank + 1)
+d.close()
+"""
+
+
+def test_bench_dist_gloo_world2(tmp_path):
+    """bench.py's multi-rank plumbing (torchrun, gloo barrier, max / sum over
+    ranks) at world size 2 on the CPU, and stdout keeps only rank 0's line
+    (gloo's connection banner is sent to stderr)."""
+    script = tmp_path / "d.py"
+    script.write_text(BENCH_DIST_WORKER % ROOT)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", "29519",
+                        str(script)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().splitlines() == ["MAX 2.5 SUM 3.0"]

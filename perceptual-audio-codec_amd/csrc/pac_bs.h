@@ -123,11 +123,12 @@ __device__ __forceinline__ void wave_spectrum_pow_short(const DS& d, const PacTa
 // the powers pw[256]: findpeaks (psychoac.py:158-191, the same floor and BW
 // slice as the long model), masker SPL, then the direct masking sum per line
 // in ascending masker order, + threshold in quiet, SPL.  mz/mS/mlev: 128
-// doubles of LDS each.  out(l, thr) for l < 256.
+// doubles of LDS each.  out(l, thr) for l < 256 in the 64-line rows whose bit
+// is set in `rows` (the others are not needed: not computed).
 template <class OUT>
 __device__ __forceinline__ void wave_threshold_short(const double* pw, const PacTables* __restrict__ T, double drop,
                                                      double* mz, double* mS, double* mlev, int* kidx, int lane,
-                                                     const OUT& out) {
+                                                     int rows, const OUT& out) {
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     int nm = 0;
 #pragma unroll
@@ -160,6 +161,7 @@ __device__ __forceinline__ void wave_threshold_short(const double* pw, const Pac
     wave_sync();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+        if (!((rows >> q) & 1)) continue;          // wave-uniform
         const int l = q * WAVE + lane;
         const double zl = T->bark_line_s[l];
         double I = 0.0;

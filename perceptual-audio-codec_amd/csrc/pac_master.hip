@@ -174,6 +174,20 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     int64_t gb;
     if (!chunk_block(src.blk_off, ck, j, &gb)) return;
     if (!(F.bsf[gb] & PAC_BS_SHORT)) return;
+    // rows (64 short lines = 256 interleaved ones) whose bands use this variant,
+    // as k_master_thr: L/R where LRMS = 0, M/S where LRMS = 1; none: the wave is done
+    int rows = 0;
+    {
+        const int want = v >= 2 ? 1 : 0;
+        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int li = 4 * (q * WAVE + lane) + k;
+            const bool need = li < lend && F.lrms[gb * PAC_NB + T->band_of_line[li]] == want;
+            if (__ballot(need)) rows |= 1 << q;
+        }
+    }
+    if (!rows) return;                                       // wave-uniform (no barriers below)
     const BlockPcm rL(locate(src, gb, 0));
     const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));
     const int o = 384 + 256 * k;
@@ -190,7 +204,7 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     };
     wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw, lane);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
-    wave_threshold_short(pw, T, v >= 4 ? 0.0 : 15.0, mz, mS, mlev, kidx, lane,
+    wave_threshold_short(pw, T, v >= 4 ? 0.0 : 15.0, mz, mS, mlev, kidx, lane, rows,
                          [&](int l, double t) { out[4 * l + k] = t; });
 }
 

@@ -250,6 +250,12 @@ static void build_tables(int fs, int window, PacTables* t) {
             if (v > mxs) mxs = v;
         }
         for (int k = 0; k < 256; k++) t->mld_s[k] = t->mld_s[k] / mxs;
+        const long double kl = (long double)(-27.0 * 0.33219280948873624);   // PAC_KL, double-rounded
+        for (int l = 0; l < 256; l++) {
+            const long double e = kl * (long double)t->bark_line_s[l];
+            t->pow_kl_s[l] = (double)exp2l(e);
+            t->pow_mkl_s[l] = (double)exp2l(-e);
+        }
     }
     for (int l = 0, ku = 0, kv = 0; l < PAC_HALFN; l++) {   // bark_line ascending in l
         const double zl = t->bark_line[l];

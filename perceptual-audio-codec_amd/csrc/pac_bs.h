@@ -119,16 +119,32 @@ __device__ __forceinline__ void wave_spectrum_pow_short(const DS& d, const PacTa
     wave_sync();
 }
 
+// exclusive prefix over the wave of per-lane pairs (elements 2 lane, 2 lane + 1)
+__device__ __forceinline__ void wave_excl_scan2(double a, double b, double* e0, double* e1) {
+    const double inc = wave_incl_scan_f64(a + b);
+    const double before = dpp_f64<PAC_DPP_WSHR1>(0.0, inc);     // the previous lanes' sum
+    *e0 = before;
+    *e1 = before + a;
+}
+
 // calcBTHR (psychoac.py:409-456) of a short block at N = 512 by one wave, from
 // the powers pw[256]: findpeaks (psychoac.py:158-191, the same floor and BW
-// slice as the long model), masker SPL, then the direct masking sum per line
-// in ascending masker order, + threshold in quiet, SPL.  mz/mS/mlev: 128
-// doubles of LDS each.  out(l, thr) for l < 256 in the 64-line rows whose bit
-// is set in `rows` (the others are not needed: not computed).
+// slice as the long model), masker SPL, then per line the masking sum of
+// psychoac.py:111-116,447-456 split by the rank bounds U(l) = #{dz > 1/2},
+// V(l) = #{dz >= -1/2} (maskers ascend in frequency) as in pac_wave.h:
+//   flat  U <= m < V:  2^B_m                        (direct, few maskers)
+//   lower m >= V:      2^(-KL z_l) * suffix sum of 2^(B_m + KL (z_m - 1/2))
+//   upper m < U, quiet (SPL <= 40: slope KL exactly):
+//                      2^(KL z_l) * prefix sum of 2^(B_m - KL (z_m + 1/2))
+//   upper m < U, loud: 2^(B_m + ku_m (z_l - z_m - 1/2)) directly
+// All terms are positive: the regrouping moves the sum by a few ulp.  Then +
+// threshold in quiet, SPL.  R: the wave's 8 KB of LDS, pw at R + 4096 (2 KB).
+// out(l, thr) for l < 256 in the 64-line rows whose bit is set in `rows`.
 template <class OUT>
-__device__ __forceinline__ void wave_threshold_short(const double* pw, const PacTables* __restrict__ T, double drop,
-                                                     double* mz, double* mS, double* mlev, int* kidx, int lane,
+__device__ __forceinline__ void wave_threshold_short(char* R, const PacTables* __restrict__ T, double drop, int lane,
                                                      int rows, const OUT& out) {
+    const double* pw = reinterpret_cast<const double*>(R + 4096);
+    int* kidx = reinterpret_cast<int*>(R + 3584);
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     int nm = 0;
 #pragma unroll
@@ -144,19 +160,75 @@ __device__ __forceinline__ void wave_threshold_short(const double* pw, const Pac
         nm += __popcll(bal);
     }
     wave_sync();
+    // per masker m = lane, 64 + lane: level, position and the factored terms,
+    // in registers until every read of pw / kidx is done
     const double csp = 8.0 / 3.0 * 4.0 / (512.0 * 512.0);
-    for (int m = lane; m < nm; m += WAVE) {
-        const int k = kidx[m];
-        double s = 0.0;
-        if (k >= 3) {
-            const int hi = k + 3 < 256 ? k + 3 : 256;
-            for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, pw[i]);
+    double z[2], B[2], ku[2], E[2], P[2], Q[2];
+    bool loud[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = h * WAVE + lane;
+        loud[h] = false;
+        z[h] = B[h] = ku[h] = E[h] = P[h] = Q[h] = 0.0;
+        if (m < nm) {
+            const int k = kidx[m];
+            double s = 0.0;
+            if (k >= 3) {
+                const int hi = k + 3 < 256 ? k + 3 : 256;
+                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, pw[i]);
+            }
+            const double sp = pac_spl(csp * s);
+            double lev = sp - 40.0;
+            lev = 0.367 * (0.0 > lev ? 0.0 : lev);
+            loud[h] = lev != 0.0;
+            z[h] = T->bark_bin_s[k];
+            B[h] = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
+            ku[h] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
+            E[h] = pac_exp2(B[h]);
+            double hh, lo;
+            dd_affine(B[h], PAC_KL, z[h], 0.5, hh, lo);          // B + KL (z - 1/2)
+            P[h] = pac_exp2_dd(hh, lo);
+            if (!loud[h]) {
+                dd_affine(B[h], PAC_KL, -0.5, z[h], hh, lo);     // B - KL (z + 1/2)
+                Q[h] = pac_exp2_dd(hh, lo);
+            }
         }
-        const double sp = pac_spl(csp * s);
-        double lev = sp - 40.0;
-        mlev[m] = 0.367 * (0.0 > lev ? 0.0 : lev);
-        mS[m] = sp;
-        mz[m] = T->bark_bin_s[k];
+    }
+    wave_sync();
+    double* Lz = reinterpret_cast<double*>(R);            // [128] masker Bark positions
+    double* LE = reinterpret_cast<double*>(R + 1024);     // [128] 2^B
+    double* LP = reinterpret_cast<double*>(R + 2048);     // [128] suffix sums of P (P then)
+    double* LQ = reinterpret_cast<double*>(R + 3080);     // [128] exclusive prefix sums of Q (Q then)
+    double* lz = reinterpret_cast<double*>(R + 4104);     // loud maskers: z, B, ku
+    double* lB = reinterpret_cast<double*>(R + 5128);
+    double* lku = reinterpret_cast<double*>(R + 6152);
+    int16_t* lpre = reinterpret_cast<int16_t*>(R + 7176); // [129] #loud maskers below m
+    int nloud = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = h * WAVE + lane;
+        Lz[m] = z[h];
+        LE[m] = E[h];
+        LP[m] = P[h];
+        LQ[m] = Q[h];
+        const unsigned long long lb = __ballot(loud[h]);
+        const int j = nloud + __popcll(lb & below);
+        lpre[m] = (int16_t)j;
+        if (loud[h]) { lz[j] = z[h]; lB[j] = B[h]; lku[j] = ku[h]; }
+        nloud += __popcll(lb);
+    }
+    wave_sync();
+    {   // pairs in masker order; the suffix of P as a prefix over the mirrored order
+        const double q0 = LQ[2 * lane], q1 = LQ[2 * lane + 1];
+        const double r0v = LP[127 - 2 * lane], r1v = LP[126 - 2 * lane];
+        double e0, e1, r0, r1;
+        wave_excl_scan2(q0, q1, &e0, &e1);
+        wave_excl_scan2(r0v, r1v, &r0, &r1);
+        wave_sync();
+        LQ[2 * lane] = e0;
+        LQ[2 * lane + 1] = e1;
+        LP[127 - 2 * lane] = r0 + r0v;
+        LP[126 - 2 * lane] = r1 + r1v;
     }
     wave_sync();
 #pragma unroll
@@ -164,15 +236,24 @@ __device__ __forceinline__ void wave_threshold_short(const double* pw, const Pac
         if (!((rows >> q) & 1)) continue;          // wave-uniform
         const int l = q * WAVE + lane;
         const double zl = T->bark_line_s[l];
-        double I = 0.0;
-        for (int m = 0; m < nm; ++m) {
-            const double dz = __dsub_rn(zl, mz[m]);
-            const double A = (dz >= 0 ? mlev[m] : 0.0) - 27.0;
-            const double ad = fabs(dz);
-            const double B = ad > 0.5 ? ad - 0.5 : 0.0;
-            const double spl = __dsub_rn(__dadd_rn(mS[m], __dmul_rn(A, B)), drop);
-            I = __dadd_rn(I, pac_exp2(__dmul_rn(__dsub_rn(spl, 96.0), PAC_LOG2_10_OVER_10)));
+        // U = #maskers with zl - z > 1/2, V = #maskers with zl - z >= -1/2
+        int U = 0, V = 0;
+#pragma unroll
+        for (int st = 64; st; st >>= 1) {
+            if (U + st <= nm && __dsub_rn(zl, Lz[U + st - 1]) > 0.5) U += st;
+            if (V + st <= nm && __dsub_rn(zl, Lz[V + st - 1]) >= -0.5) V += st;
         }
-        out(l, pac_spl(__dadd_rn(I, T->tiq_s[l])));
+        double flat = 0.0;
+        for (int m = U; m < V; ++m) flat += LE[m];
+        const double lower = (V < nm ? LP[V] : 0.0) * T->pow_mkl_s[l];
+        const double upq = LQ[U] * T->pow_kl_s[l];
+        const int Ul = U < nm ? lpre[U] : nloud;
+        const int umax = wave_max_i(Ul);
+        double up = 0.0;
+        for (int j = 0; j < umax; ++j) {
+            const double t = pac_exp2(__builtin_fma(__dsub_rn(zl, lz[j]) - 0.5, lku[j], lB[j]));
+            up += j < Ul ? t : 0.0;
+        }
+        out(l, pac_spl((((up + upq) + flat) + lower) + T->tiq_s[l]));
     }
 }

@@ -63,6 +63,7 @@ struct PacTables {
     double2 mdct_pre_s[128];          // exp(-i pi (q+1/4)/256)
     double2 mdct_post_s[128];         // exp(-i pi q / 256)
     double bark_line_s[256], tiq_s[256], bark_bin_s[256], mld_s[256];
+    double pow_kl_s[256], pow_mkl_s[256];   // 2^(KL z_l), 2^(-KL z_l) of the short lines
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

@@ -159,14 +159,10 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
                                                           PacMasterChunkBuf K, PacMasterFields F,
                                                           PacMasterChunk ck) {
     // per wave (8 KB): FFT buffer + scratch; then the powers in the scratch and
-    // the masker list in the FFT buffer
+    // the masker lists over the whole 8 KB (wave_threshold_short)
     __shared__ double2 bufs[4][2][256];
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), k = tid / WAVE;
-    double* pw = reinterpret_cast<double*>(bufs[k][1]);
-    double* mz = reinterpret_cast<double*>(bufs[k][0]);
-    double* mS = mz + 128;
-    double* mlev = mz + 256;
-    int* kidx = reinterpret_cast<int*>(mz + 384);
+    double* pw = reinterpret_cast<double*>(bufs[k][1]);      // = wave region + 4096
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
     const int nvar = ck.nch == 2 ? 6 : 1;
     const int64_t j = item / nvar;
@@ -204,7 +200,7 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     };
     wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw, lane);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
-    wave_threshold_short(pw, T, v >= 4 ? 0.0 : 15.0, mz, mS, mlev, kidx, lane, rows,
+    wave_threshold_short(reinterpret_cast<char*>(bufs[k][0]), T, v >= 4 ? 0.0 : 15.0, lane, rows,
                          [&](int l, double t) { out[4 * l + k] = t; });
 }
 

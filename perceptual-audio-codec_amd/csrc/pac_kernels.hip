@@ -56,6 +56,19 @@ __device__ __forceinline__ BlockRef locate(const PacSource& src, int64_t gb, int
     r.n_frames = src.frame_off[s + 1] - f0;
     return r;
 }
+// the same for a block whose stream s and index b in it are known (no search)
+__device__ __forceinline__ BlockRef locate_sb(const PacSource& src, int s, int64_t b, int64_t gb, int c) {
+    if (src.fsrc) return locate(src, gb, c);
+    BlockRef r;
+    r.nch = src.n_ch;
+    r.c = c;
+    const int64_t f0 = src.frame_off[s];
+    r.pcm = src.pcm + f0 * src.n_ch;
+    r.fsrc = nullptr;
+    r.first_frame = (b - 1) * PAC_HALFN + (src.lead ? src.lead[s] : 0);
+    r.n_frames = src.frame_off[s + 1] - f0;
+    return r;
+}
 
 // raw signed-fraction sample i (0..2047) of the block: prior hop ++ current
 // hop (pacfile.py:279-282), zero outside the stream (pcmfile.py:77-79, the

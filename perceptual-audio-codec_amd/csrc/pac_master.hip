@@ -61,14 +61,18 @@ struct PacMasterChunk {
     int nch;        // 2, or 1 for the mono master extension (no LRMS, one threshold)
 };
 
-// global block id of local block j, false if that stream has ended
+// global block id of local block j (and its stream, index in the stream),
+// false if that stream has ended
+struct ChunkPos { int64_t gb, t; int s; };
 __device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off, const PacMasterChunk& ck,
-                                            int64_t j, int64_t* gb) {
+                                            int64_t j, ChunkPos* cp) {
     const int s = ck.s_first + (int)(j / ck.S);
     const int64_t t = ck.t0 + j % ck.S;
     const int64_t b0 = blk_off[s];
     if (t >= blk_off[s + 1] - b0) return false;
-    *gb = b0 + t;
+    cp->gb = b0 + t;
+    cp->t = t;
+    cp->s = s;
     return true;
 }
 
@@ -102,8 +106,9 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const int nvar = ck.nch == 2 ? 6 : 1;      // mono master: BTHR_L only
     const int64_t j = item / nvar;             // block within the chunk
     const int v = (int)(item % nvar);
-    int64_t gb;
-    if (!chunk_block(src.blk_off, ck, j, &gb)) return;     // uniform per workgroup
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;     // uniform per workgroup
+    const int64_t gb = cp.gb;
     const int fl = F.bsf ? F.bsf[gb] : 0;
     if (fl & PAC_BS_SHORT) return;                          // k_master_thr_short's
     // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
@@ -127,8 +132,8 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     __syncthreads();
     const int rows = rowmask;
     if (!rows) return;                                      // uniform per workgroup
-    const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
+    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
     auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
     grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
     const MaskerLists L = masker_lists(buf, tmp);
@@ -167,8 +172,9 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     const int nvar = ck.nch == 2 ? 6 : 1;
     const int64_t j = item / nvar;
     const int v = (int)(item % nvar);
-    int64_t gb;
-    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
+    const int64_t gb = cp.gb;
     if (!(F.bsf[gb] & PAC_BS_SHORT)) return;
     // rows (64 short lines = 256 interleaved ones) whose bands use this variant,
     // as k_master_thr: L/R where LRMS = 0, M/S where LRMS = 1; none: the wave is done
@@ -184,8 +190,8 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
         }
     }
     if (!rows) return;                                       // wave-uniform (no barriers below)
-    const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, ck.nch == 2 ? 1 : 0));
+    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));
     const int o = 384 + 256 * k;
     auto d = [&](int i) {
         const double h = T->hann_s[i], w = T->sine_s[i];
@@ -378,10 +384,11 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
-    int64_t gb;
-    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
-    const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, 1));
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
+    const int64_t gb = cp.gb;
+    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
     grp_spectrum_cplx2<256>([&](int i) { return rL(i); }, [&](int i) { return rR(i); }, T, bufA, bufB, tid);
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
@@ -460,13 +467,14 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     uint8_t* lrms_s = reinterpret_cast<uint8_t*>(bufB + 640);
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
-    int64_t gb;
-    if (!chunk_block(src.blk_off, ck, j, &gb)) return;
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
+    const int64_t gb = cp.gb;
     const bool st = ck.nch == 2;                 // mono master: channel 0 alone, LRMS all 0
     const int fl = F.bsf ? F.bsf[gb] : 0;        // block-switching flags (pac_bs.h), 0: off
     const bool sh = fl & PAC_BS_SHORT;
-    const BlockPcm rL(locate(src, gb, 0));
-    const BlockPcm rR(locate(src, gb, st ? 1 : 0));
+    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
     const double* XL;

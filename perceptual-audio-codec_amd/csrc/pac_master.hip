@@ -79,6 +79,18 @@ __device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off,
 // LRMS-variant signals: the in-place window chains of EncodeDualChannel and
 // getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
 // M = (a+b)/2, S = (a-b)/2; v2 = M*hann, v3 = S*hann, v4 = (M*hann)*hann, ...
+// the variant chain from the two channels' samples xl, xr, window w, Hann h
+__device__ __forceinline__ double variant_from(double xl, double xr, double w, double h, int v) {
+    if (v == 1) return __dmul_rn(__dmul_rn(xr, w), h);
+    const double a = __dmul_rn(__dmul_rn(xl, w), h);
+    if (v == 0) return a;
+    const double b = __dmul_rn(__dmul_rn(xr, w), h);
+    double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
+    ms = __dmul_rn(ms, h);
+    if (v >= 4) ms = __dmul_rn(ms, h);
+    return ms;
+}
+
 // fl: block-switching flags of a long frame (the MDCT window's start / stop
 // shapes, pac_bs.h), 0 = the plain window
 __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const BlockPcm& rR,
@@ -134,8 +146,35 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     if (!rows) return;                                      // uniform per workgroup
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
-    auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
-    grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
+    if (ck.nch == 2 && !rL.f) {
+        // stereo PCM: both channels of a frame in one 32-bit load, the window
+        // tables as double2 -- the samples of variant_sample, fewer loads
+        auto dp = [&](int n) {
+            const int i0 = 2 * n;
+            int c[4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int i = i0 + u;
+                uint32_t wv = 0u;
+                if (i >= rL.ilo && i < rL.ihi) wv = *reinterpret_cast<const uint32_t*>(rL.p + 2 * (i - rL.ilo));
+                c[2 * u] = (int)(int16_t)(wv & 0xffffu);
+                c[2 * u + 1] = (int)(int16_t)(wv >> 16);
+            }
+            const double2 h = *reinterpret_cast<const double2*>(T->hann + i0);
+            const double2 w = fl ? make_double2(bs_long_win(T, fl, i0), bs_long_win(T, fl, i0 + 1))
+                                 : *reinterpret_cast<const double2*>(T->sine + i0);
+            double r[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                r[u] = variant_from(pac_pcm_to_float(c[2 * u]), pac_pcm_to_float(c[2 * u + 1]), u ? w.y : w.x,
+                                    u ? h.y : h.x, v);
+            return make_double2(r[0], r[1]);
+        };
+        grp_spectrum_pow_pairs<FRONT_NT>(dp, T, buf, tmp, tid);
+    } else {
+        auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
+        grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
+    }
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;

@@ -466,13 +466,14 @@ __device__ __forceinline__ void grp_mdct2(const FA& xa, const FB& xb, const PacT
 // pairs are staged in buf, the FFT ends in tmp, and on return
 // buf[k].x = Re^2 + Im^2 (tmp is free again).  (findpeaks compares |X| and
 // the masker SPL sums |X|^2 (psychoac.py:442-449); both only need the square.)
-template <int NT, class DS>
-__device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
-                                                 double2* buf, double2* tmp, int tid) {
+// (grp_spectrum_pow_pairs: the staged pairs come from dp(n) = (d(2n), d(2n+1)).)
+template <int NT, class DP>
+__device__ __forceinline__ void grp_spectrum_pow_pairs(const DP& dp, const PacTables* __restrict__ T,
+                                                       double2* buf, double2* tmp, int tid) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
-        int n = n0 + tid;
-        buf[n] = make_double2(d(2 * n), d(2 * n + 1));
+        const int n = n0 + tid;
+        buf[n] = dp(n);
     }
     const double2* Z = grp_fft_stockham<10, NT>(buf, tmp, T->fft_tw, tid);   // = tmp
     // split: X[k] = (Z[k] + conj Z[M-k])/2 - i/2 W^k (Z[k] - conj Z[M-k]).
@@ -496,6 +497,11 @@ __device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* _
         }
     }
     grp_sync<NT>();
+}
+template <int NT, class DS>
+__device__ __forceinline__ void grp_spectrum_pow(const DS& d, const PacTables* __restrict__ T,
+                                                 double2* buf, double2* tmp, int tid) {
+    grp_spectrum_pow_pairs<NT>([&](int n) { return make_double2(d(2 * n), d(2 * n + 1)); }, T, buf, tmp, tid);
 }
 
 // one-wave aliases used by the single-wave kernels

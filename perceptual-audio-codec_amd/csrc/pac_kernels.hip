@@ -70,6 +70,12 @@ __device__ __forceinline__ BlockRef locate_sb(const PacSource& src, int s, int64
     return r;
 }
 
+// stereo frame i (0..2047) of a block as the two channels' sample codes, one
+// 32-bit load (r: the channel-0 BlockPcm of an interleaved stereo source);
+// zero outside the stream
+struct BlockPcm;
+__device__ __forceinline__ double2 stereo_frame(const BlockPcm& r, int i);
+
 // raw signed-fraction sample i (0..2047) of the block: prior hop ++ current
 // hop (pacfile.py:279-282), zero outside the stream (pcmfile.py:77-79, the
 // zero first prior block pacfile.py:265-268 and the Close() flush block)
@@ -103,6 +109,11 @@ struct BlockPcm {
         return pac_pcm_to_float(c);
     }
 };
+__device__ __forceinline__ double2 stereo_frame(const BlockPcm& r, int i) {
+    uint32_t w = 0u;
+    if (i >= r.ilo && i < r.ihi) w = *reinterpret_cast<const uint32_t*>(r.p + 2 * (i - r.ilo));
+    return make_double2(pac_pcm_to_float((int)(int16_t)(w & 0xffffu)), pac_pcm_to_float((int)(int16_t)(w >> 16)));
+}
 
 // xs[i] = x(i) * sine[i] (window.py:27-39, codec.py:240) into LDS, i < 2048
 template <int NT>

@@ -378,14 +378,16 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 
 // the complex spectra of two real 2048-blocks dA, dB at once (as
 // grp_spectrum_cplx on each: bit-identical), both FFTs stage by stage together
-template <int NT, class DA, class DB>
-__device__ __forceinline__ void grp_spectrum_cplx2(const DA& dA, const DB& dB, const PacTables* __restrict__ T,
-                                                   double2* bufA, double2* bufB, int tid) {
+// (d4(n) = (dA(2n), dA(2n+1), dB(2n), dB(2n+1)): the staged pairs of both)
+template <int NT, class D4>
+__device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
+                                                    double2* bufA, double2* bufB, int tid) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
         const int n = n0 + tid;
-        bufA[n] = make_double2(dA(2 * n), dA(2 * n + 1));
-        bufB[n] = make_double2(dB(2 * n), dB(2 * n + 1));
+        const double4 v = d4(n);
+        bufA[n] = make_double2(v.x, v.y);
+        bufB[n] = make_double2(v.z, v.w);
     }
     grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid);
 #pragma unroll
@@ -428,7 +430,16 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     const int64_t gb = cp.gb;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
-    grp_spectrum_cplx2<256>([&](int i) { return rL(i); }, [&](int i) { return rR(i); }, T, bufA, bufB, tid);
+    if (!rL.f) {
+        grp_spectrum_cplx2p<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
+            const double2 f0 = stereo_frame(rL, 2 * n), f1 = stereo_frame(rL, 2 * n + 1);
+            return make_double4(f0.x, f1.x, f0.y, f1.y);
+        }, T, bufA, bufB, tid);
+    } else {
+        grp_spectrum_cplx2p<256>([&](int n) {
+            return make_double4(rL(2 * n), rL(2 * n + 1), rR(2 * n), rR(2 * n + 1));
+        }, T, bufA, bufB, tid);
+    }
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
@@ -529,8 +540,18 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
         if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid);
     } else if (st) {   // both channels' MDCTs stage by stage together
-        grp_mdct2<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); },
-                       [&](int i) { return __dmul_rn(rR(i), T->sine[i]); }, T, bufA, bufB, tid);
+        if (!rL.f) {
+            grp_mdct2<256>([&](int i) {
+                const double2 x = stereo_frame(rL, i);
+                const double w = T->sine[i];
+                return make_double2(__dmul_rn(x.x, w), __dmul_rn(x.y, w));
+            }, T, bufA, bufB, tid);
+        } else {
+            grp_mdct2<256>([&](int i) {
+                const double w = T->sine[i];
+                return make_double2(__dmul_rn(rL(i), w), __dmul_rn(rR(i), w));
+            }, T, bufA, bufB, tid);
+        }
         XL = reinterpret_cast<const double*>(bufA);
         XR = reinterpret_cast<const double*>(bufB);
     } else {

@@ -422,21 +422,26 @@ __device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __res
 }
 
 // Two MDCTs at once (grp_mdct of xa into bufA and of xb into bufB, FFTs
-// stage by stage together): bit-identical to two grp_mdct calls.
-template <int NT, class FA, class FB>
-__device__ __forceinline__ void grp_mdct2(const FA& xa, const FB& xb, const PacTables* __restrict__ T,
+// stage by stage together; xab(i) = (xa(i), xb(i)) so a stereo source loads
+// each frame once): bit-identical to two grp_mdct calls.
+template <int NT, class FAB>
+__device__ __forceinline__ void grp_mdct2(const FAB& xab, const PacTables* __restrict__ T,
                                           double2* bufA, double2* bufB, int tid) {
-    auto folda = [&](int n) {
-        return n < 512 ? __dsub_rn(-xa(1535 - n), xa(1536 + n)) : __dsub_rn(xa(n - 512), xa(1535 - n));
-    };
-    auto foldb = [&](int n) {
-        return n < 512 ? __dsub_rn(-xb(1535 - n), xb(1536 + n)) : __dsub_rn(xb(n - 512), xb(1535 - n));
+    // xab(i) = (xa(i), xb(i)): the two windowed samples at i
+    auto fold = [&](int n) {
+        if (n < 512) {
+            const double2 u = xab(1535 - n), w = xab(1536 + n);
+            return make_double2(__dsub_rn(-u.x, w.x), __dsub_rn(-u.y, w.y));
+        }
+        const double2 u = xab(n - 512), w = xab(1535 - n);
+        return make_double2(__dsub_rn(u.x, w.x), __dsub_rn(u.y, w.y));
     };
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
         const int q = q0 + tid;
-        bufA[q] = cmul(make_double2(folda(2 * q), folda(1023 - 2 * q)), T->mdct_pre[q]);
-        bufB[q] = cmul(make_double2(foldb(2 * q), foldb(1023 - 2 * q)), T->mdct_pre[q]);
+        const double2 f0 = fold(2 * q), f1 = fold(1023 - 2 * q);
+        bufA[q] = cmul(make_double2(f0.x, f1.x), T->mdct_pre[q]);
+        bufB[q] = cmul(make_double2(f0.y, f1.y), T->mdct_pre[q]);
     }
     double2 *Ya, *Yb;
     grp_fft_stockham_x2<9, NT>(bufA, bufA + 512, bufB, bufB + 512, T->fft_tw, tid, &Ya, &Yb);   // = buf + 512

@@ -146,7 +146,8 @@ REF_ALG_FLOP_PER_BLOCK = {"origin": 18.0e6, "master": 48.0e6}
 # what the kernel must read and write, not what it happens to move.
 ALG_BYTES = {
     "k_origin_front": 4096 + 2 * (25 * 8 * 2 + 1),   # int16 PCM in; SMR + band peaks + overall out
-    "k_master_thr": 4096 + 6 * 1024 * 8,             # int16 PCM in; 6 threshold rows out (calcBTHR x 6)
+    "k_master_spec": 4096 + 2 * 1025 * 16,           # int16 PCM in; FFT bins 0..1024 of a and b out
+    "k_master_thr": 2 * 1025 * 16 + 6 * 1024 * 8,    # the spectra in; 6 threshold rows out (calcBTHR x 6)
     "k_master_front": 4096 + 6 * 1024 * 8 + 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2,
     "k_master_tail": 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2 * (25 * 2 + 1 + 4 + 8),
     "k_master_pack": 2 * 1024 * 8 + 2 * 25 * 2 + 25 + 2 + 2 * 300,
@@ -461,7 +462,8 @@ def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a):
 PHASES = {  # pac_timing field -> kernel, per profile (include/pac_gpu.h)
     "origin": [("front_ms", "k_origin_front"), ("alloc_ms", "k_origin_alloc"), ("scan_ms", "k_scan"),
                ("pack_ms", "k_origin_pack")],
-    "master": [("lrms_ms", "k_master_lrms"), ("thr_ms", "k_master_thr"), ("front_ms", "k_master_front"),
+    "master": [("lrms_ms", "k_master_lrms"), ("spec_ms", "k_master_spec"), ("thr_ms", "k_master_thr"),
+               ("front_ms", "k_master_front"),
                ("alloc_ms", "k_master_tail"),
                ("pack_ms", "k_master_pack"), ("scan_ms", "k_scan")],
 }

@@ -88,7 +88,7 @@ typedef struct {
  * context's stream around each launch, read after the call), ms.
  *   origin: front = k_origin_front, alloc = k_origin_alloc, scan = k_scan_*,
  *           pack = k_origin_pack, thr = 0
- *   master: lrms = k_master_lrms, thr = k_master_thr, front = k_master_front,
+ *   master: lrms = k_master_lrms, spec = k_master_spec, thr = k_master_thr, front = k_master_front,
  *           alloc = k_master_tail (second stream, overlapping the next chunk),
  *           scan = k_scan_*, pack = k_master_pack (each summed over the chunks) */
 typedef struct {
@@ -96,12 +96,13 @@ typedef struct {
     float alloc_ms;
     float scan_ms;
     float pack_ms;
-    float total_ms;     /* origin: first to last event; master: lrms+thr(+thr_short)+front+scan+pack */
+    float total_ms;     /* origin: first to last event; master: lrms+spec+thr(+thr_short)+front+scan+pack */
     int64_t n_channel_blocks;
     int64_t out_bytes;
     float thr_ms;
     float lrms_ms;
     float thr_short_ms; /* block switching: k_master_thr_short (the short frames' thresholds) */
+    float spec_ms;      /* master: k_master_spec (the windowed L/R spectra the thresholds derive from) */
 } pac_timing;
 
 /* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */

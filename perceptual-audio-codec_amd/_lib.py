@@ -54,7 +54,8 @@ class Timing(C.Structure):
     _fields_ = [("front_ms", C.c_float), ("alloc_ms", C.c_float), ("scan_ms", C.c_float),
                 ("pack_ms", C.c_float), ("total_ms", C.c_float),
                 ("n_channel_blocks", C.c_int64), ("out_bytes", C.c_int64),
-                ("thr_ms", C.c_float), ("lrms_ms", C.c_float), ("thr_short_ms", C.c_float)]
+                ("thr_ms", C.c_float), ("lrms_ms", C.c_float), ("thr_short_ms", C.c_float),
+                ("spec_ms", C.c_float)]
 
 
 class BlockFields(C.Structure):

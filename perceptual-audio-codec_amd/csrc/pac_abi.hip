@@ -316,6 +316,7 @@ struct pac_ctx {
     DevBuf<double> fsrc;
     // master
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
+    DevBuf<double2> m_spec;               // [chunk][2][PAC_SPEC_LD] k_master_spec -> k_master_thr
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
     DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack)
     DevBuf<int64_t> st_extra, st_deposit;
@@ -393,7 +394,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     for (auto& kv : c->tables) hipFree(kv.second);
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
-    c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release();
+    c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
     c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
@@ -721,6 +722,7 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     c->last.thr_ms = 0.f;
     c->last.lrms_ms = 0.f;
     c->last.thr_short_ms = 0.f;
+    c->last.spec_ms = 0.f;
     hipEventSynchronize(c->ev[4]);
     hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
     hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
@@ -772,7 +774,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_lines.ensure(2 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(2 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(2 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(2 * cbmax * 2 * PAC_NB)))
         return rc;
     if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
@@ -821,7 +823,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             const int k = (int)(i & 1);
             const PacMasterChunk ck{gr.g0, gr.n_s, t0, gr.S, nch};
             const PacMasterChunkBuf K{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
-                                      c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB};
+                                      c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
+                                      c->m_spec.p};
             const int64_t B = (int64_t)gr.n_s * gr.S;
             if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
             if (lrms_async) {
@@ -840,6 +843,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                     hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
                 if ((rc = mark(0, 5))) return rc;
             }
+            hipLaunchKernelGGL(k_master_spec, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
+            if ((rc = mark(0, 7))) return rc;
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
             if ((rc = mark(0, 0))) return rc;
             if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
@@ -879,7 +884,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s0));
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
-        float ph[7] = {0, 0, 0, 0, 0, 0, 0};
+        float ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < 3; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
@@ -894,7 +899,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         c->last.scan_ms = ph[4];
         c->last.lrms_ms = ph[5];
         c->last.thr_short_ms = ph[6];
-        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5] + ph[6];   // the tail overlaps the next chunk
+        c->last.spec_ms = ph[7];
+        c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5] + ph[6] + ph[7];   // the tail overlaps the next chunk
         c->last.n_channel_blocks = G;
         c->last.out_bytes = 0;
     }

@@ -33,7 +33,9 @@ struct PacMasterChunkBuf {
     double* lines;      // [Bc][2][1024]  LRMSmdctLines
     double* smr;        // [Bc][2][25]
     double* bandpeak;   // [Bc][2][25]    max |line| per band
+    double2* spec;      // [Bc][2][PAC_SPEC_LD] FFT bins 0..1024 of a and b (k_master_spec)
 };
+#define PAC_SPEC_LD 1040    // double2 per spectrum: bins 0..1024, padded to 256 B
 
 // per-call fields; channel-block g = nch gb + ch (gb = global block, file order)
 struct PacMasterFields {
@@ -79,18 +81,6 @@ __device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off,
 // LRMS-variant signals: the in-place window chains of EncodeDualChannel and
 // getStereoMaskThreshold.  a = (x_L*sine)*hann, b = (x_R*sine)*hann;
 // M = (a+b)/2, S = (a-b)/2; v2 = M*hann, v3 = S*hann, v4 = (M*hann)*hann, ...
-// the variant chain from the two channels' samples xl, xr, window w, Hann h
-__device__ __forceinline__ double variant_from(double xl, double xr, double w, double h, int v) {
-    if (v == 1) return __dmul_rn(__dmul_rn(xr, w), h);
-    const double a = __dmul_rn(__dmul_rn(xl, w), h);
-    if (v == 0) return a;
-    const double b = __dmul_rn(__dmul_rn(xr, w), h);
-    double ms = ((v & 1) == 0) ? __dadd_rn(a, b) / 2.0 : __dsub_rn(a, b) / 2.0;
-    ms = __dmul_rn(ms, h);
-    if (v >= 4) ms = __dmul_rn(ms, h);
-    return ms;
-}
-
 // fl: block-switching flags of a long frame (the MDCT window's start / stop
 // shapes, pac_bs.h), 0 = the plain window
 __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const BlockPcm& rR,
@@ -105,6 +95,58 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
     ms = __dmul_rn(ms, h);
     if (v >= 4) ms = __dmul_rn(ms, h);
     return ms;
+}
+
+// The six variants' spectra from A = FFT(a), B = FFT(b) (bins 0..1024,
+// X[-k] = conj X[k], X[2048-k] = conj X[k] for the real blocks): the M/S
+// signals are (a +- b)/2 and an in-place Hann multiply (window.py:41-53,
+// h[n] = (1 - cos(2 pi (n + 1/2)/N))/2) is, on the spectrum, the 3-tap
+//   FFT(x h)[k] = X[k]/2 - e^{i pi/N} X[k-1]/4 - e^{-i pi/N} X[k+1]/4
+// (v2 = M h, v3 = S h: one tap; v4 = M h h, v5 = S h h: two).  The same
+// values as a direct FFT of the windowed signal up to rounding of the
+// FFT's own order (bins within ~1e-16 of the spectrum's maximum).
+#define PAC_HANN_C 0.9999988234517019      // cos(pi / 2048)
+#define PAC_HANN_S 0.0015339801862847655   // sin(pi / 2048)
+__device__ __forceinline__ double2 spec_at(const double2* __restrict__ S, int k) {
+    const int kk = k < 0 ? -k : (k > 1024 ? 2048 - k : k);
+    double2 x = S[kk];
+    if (kk != k) x.y = -x.y;
+    return x;
+}
+__device__ __forceinline__ double2 hann_tap(double2 xm, double2 x0, double2 xp) {
+    const double mr = PAC_HANN_C * xm.x - PAC_HANN_S * xm.y, mi = PAC_HANN_C * xm.y + PAC_HANN_S * xm.x;
+    const double pr = PAC_HANN_C * xp.x + PAC_HANN_S * xp.y, pi = PAC_HANN_C * xp.y - PAC_HANN_S * xp.x;
+    return make_double2(0.5 * x0.x - 0.25 * (mr + pr), 0.5 * x0.y - 0.25 * (mi + pi));
+}
+// buf[k].x = |V_v[k]|^2, k < 1024; S = the block's spectra (A at S, B at
+// S + PAC_SPEC_LD).  Each thread owns 4 consecutive bins (8 loads of the
+// neighbourhood instead of 5 per bin).
+template <int NT>
+__device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, int v, double2* buf, int tid) {
+    static_assert(NT * 4 == 1024, "4 bins per thread");
+    const int k0 = 4 * tid;
+    double2 X[4];
+    if (v < 2) {
+        const double2* P = S + (v ? PAC_SPEC_LD : 0) + k0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[i] = P[i];
+    } else {
+        const double sg = (v & 1) ? -1.0 : 1.0;      // M = (a + b)/2, S = (a - b)/2
+        double2 m[8];                                // bins k0 - 2 .. k0 + 5
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double2 a = spec_at(S, k0 - 2 + i), b = spec_at(S + PAC_SPEC_LD, k0 - 2 + i);
+            m[i] = make_double2(0.5 * (a.x + sg * b.x), 0.5 * (a.y + sg * b.y));
+        }
+        double2 h[6];                                // M h at bins k0 - 1 .. k0 + 4
+#pragma unroll
+        for (int i = 0; i < 6; ++i) h[i] = hann_tap(m[i], m[i + 1], m[i + 2]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[i] = v < 4 ? h[i + 1] : hann_tap(h[i], h[i + 1], h[i + 2]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf[k0 + i].x = __builtin_fma(X[i].x, X[i].x, X[i].y * X[i].y);
+    grp_sync<NT>();
 }
 
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
@@ -144,37 +186,8 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     __syncthreads();
     const int rows = rowmask;
     if (!rows) return;                                      // uniform per workgroup
-    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
-    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // (mono: never read, v == 0)
-    if (ck.nch == 2 && !rL.f) {
-        // stereo PCM: both channels of a frame in one 32-bit load, the window
-        // tables as double2 -- the samples of variant_sample, fewer loads
-        auto dp = [&](int n) {
-            const int i0 = 2 * n;
-            int c[4];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int i = i0 + u;
-                uint32_t wv = 0u;
-                if (i >= rL.ilo && i < rL.ihi) wv = *reinterpret_cast<const uint32_t*>(rL.p + 2 * (i - rL.ilo));
-                c[2 * u] = (int)(int16_t)(wv & 0xffffu);
-                c[2 * u + 1] = (int)(int16_t)(wv >> 16);
-            }
-            const double2 h = *reinterpret_cast<const double2*>(T->hann + i0);
-            const double2 w = fl ? make_double2(bs_long_win(T, fl, i0), bs_long_win(T, fl, i0 + 1))
-                                 : *reinterpret_cast<const double2*>(T->sine + i0);
-            double r[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-                r[u] = variant_from(pac_pcm_to_float(c[2 * u]), pac_pcm_to_float(c[2 * u + 1]), u ? w.y : w.x,
-                                    u ? h.y : h.x, v);
-            return make_double2(r[0], r[1]);
-        };
-        grp_spectrum_pow_pairs<FRONT_NT>(dp, T, buf, tmp, tid);
-    } else {
-        auto d = [&](int i) { return variant_sample(rL, rR, T, v, i, fl); };
-        grp_spectrum_pow<FRONT_NT>(d, T, buf, tmp, tid);
-    }
+    // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
+    grp_variant_pow<FRONT_NT>(K.spec + j * 2 * PAC_SPEC_LD, v, buf, tid);
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
@@ -379,9 +392,10 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 // the complex spectra of two real 2048-blocks dA, dB at once (as
 // grp_spectrum_cplx on each: bit-identical), both FFTs stage by stage together
 // (d4(n) = (dA(2n), dA(2n+1), dB(2n), dB(2n+1)): the staged pairs of both)
-template <int NT, class D4>
+template <int NT, bool NYQ = false, class D4>
 __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
-                                                    double2* bufA, double2* bufB, int tid) {
+                                                    double2* bufA, double2* bufB, int tid,
+                                                    double* nyq = nullptr) {
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
         const int n = n0 + tid;
@@ -409,6 +423,7 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
                 const double2 wo = cmul(T->rfft_tw[kk[side]], o);
                 X[side] = make_double2(e.x + wo.y, e.y - wo.x);
             }
+            if (NYQ && p == 0) nyq[u] = Z[0].x - Z[0].y;   // X[1024] = sum_even - sum_odd
             Z[kk[0]] = X[0];
             Z[kk[1]] = X[1];
         }
@@ -500,6 +515,52 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
         const double2 sd = np_csum_combine<5>(leafv0, i0, n);
         const double2 ss = np_csum_combine<5>(leafv1, i1, n);
         F.lrms[gb * PAC_NB + tid] = (uint8_t)(hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0);
+    }
+}
+
+// One 256-thread workgroup per stereo block: the complex spectra A = FFT(a),
+// B = FFT(b), bins 0..1024, of the two channels' windowed blocks
+// a = (x_L w) hann, b = (x_R w) hann (the first in-place chains of
+// EncodeDualChannel / calcBTHR, psychoac.py:540-545) -> K.spec, from which
+// k_master_thr derives all six threshold variants' spectra (grp_variant_pow).
+__global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTables* __restrict__ T,
+                                                     PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
+    __shared__ double nyq[2];
+    const int tid = threadIdx.x;
+    const int64_t j = blockIdx.x;
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
+    const int64_t gb = cp.gb;
+    const int fl = F.bsf ? F.bsf[gb] : 0;
+    if (fl & PAC_BS_SHORT) return;                 // k_master_thr_short's
+    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // mono: B = A, unused
+    if (ck.nch == 2 && !rL.f) {
+        grp_spectrum_cplx2p<256, true>([&](int n) {   // frames 2n, 2n+1 of both channels, one load each
+            const int i0 = 2 * n;
+            const double2 f0 = stereo_frame(rL, i0), f1 = stereo_frame(rL, i0 + 1);
+            const double2 h = *reinterpret_cast<const double2*>(T->hann + i0);
+            const double2 w = fl ? make_double2(bs_long_win(T, fl, i0), bs_long_win(T, fl, i0 + 1))
+                                 : *reinterpret_cast<const double2*>(T->sine + i0);
+            return make_double4(__dmul_rn(__dmul_rn(f0.x, w.x), h.x), __dmul_rn(__dmul_rn(f1.x, w.y), h.y),
+                                __dmul_rn(__dmul_rn(f0.y, w.x), h.x), __dmul_rn(__dmul_rn(f1.y, w.y), h.y));
+        }, T, bufA, bufB, tid, nyq);
+    } else {
+        grp_spectrum_cplx2p<256, true>([&](int n) {
+            return make_double4(variant_sample(rL, rR, T, 0, 2 * n, fl), variant_sample(rL, rR, T, 0, 2 * n + 1, fl),
+                                variant_sample(rL, rR, T, 1, 2 * n, fl), variant_sample(rL, rR, T, 1, 2 * n + 1, fl));
+        }, T, bufA, bufB, tid, nyq);
+    }
+    double2* o = K.spec + j * 2 * PAC_SPEC_LD;
+#pragma unroll
+    for (int k = tid; k < 1024; k += 256) {
+        o[k] = bufA[k];
+        o[PAC_SPEC_LD + k] = bufB[k];
+    }
+    if (tid == 0) {
+        o[1024] = make_double2(nyq[0], 0.0);
+        o[PAC_SPEC_LD + 1024] = make_double2(nyq[1], 0.0);
     }
 }
 

@@ -845,7 +845,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             }
             hipLaunchKernelGGL(k_master_spec, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             if ((rc = mark(0, 7))) return rc;
-            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * nvar)), dim3(FRONT_NT), 0, s0, src, T, K, F, ck);
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
+                               T, K, F, ck);
             if ((rc = mark(0, 0))) return rc;
             if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
                 hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(B * nvar)), dim3(256), 0, s0, src, T, K, F,

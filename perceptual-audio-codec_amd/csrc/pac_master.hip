@@ -149,48 +149,16 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
     grp_sync<NT>();
 }
 
-__global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                         PacMasterChunkBuf K, PacMasterFields F,
-                                                         PacMasterChunk ck) {
-    __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
-    __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // FFT scratch, then loud list (region B)
-    const int tid = threadIdx.x;
+// one threshold variant of a block (k_master_thr): |V|^2 from the block's
+// spectra, maskers, the rows the variant's bands use.
+__device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double2* __restrict__ spec,
+                                         double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
+                                         int tid) {
     const int lane = tid & (WAVE - 1);
-    const int64_t item = xcd_item(blockIdx.x, gridDim.x);
-    const int nvar = ck.nch == 2 ? 6 : 1;      // mono master: BTHR_L only
-    const int64_t j = item / nvar;             // block within the chunk
-    const int v = (int)(item % nvar);
-    ChunkPos cp;
-    if (!chunk_block(src.blk_off, ck, j, &cp)) return;     // uniform per workgroup
-    const int64_t gb = cp.gb;
-    const int fl = F.bsf ? F.bsf[gb] : 0;
-    if (fl & PAC_BS_SHORT) return;                          // k_master_thr_short's
-    // rows whose lines' bands use this variant: L/R (v < 2) where LRMS = 0,
-    // the M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
-    // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
-    int& rowmask = reinterpret_cast<int*>(tmp)[0];          // region B is idle until the spectrum
-    if (tid == 0) rowmask = 0;
-    __syncthreads();
-    {
-        const int want = v >= 2 ? 1 : 0;
-        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-        int bits = 0;
-#pragma unroll
-        for (int i = 0; i < PAC_HALFN / FRONT_NT; ++i) {
-            const int l = i * FRONT_NT + tid;
-            if (l < lend && F.lrms[gb * PAC_NB + T->band_of_line[l]] == want) bits |= 1 << (l / WAVE);
-        }
-        bits = __builtin_amdgcn_readfirstlane(wave_or_i(bits));
-        if (lane == 0 && bits) atomicOr(&rowmask, bits);
-    }
-    __syncthreads();
-    const int rows = rowmask;
-    if (!rows) return;                                      // uniform per workgroup
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
-    grp_variant_pow<FRONT_NT>(K.spec + j * 2 * PAC_SPEC_LD, v, buf, tid);
+    grp_variant_pow<FRONT_NT>(spec, v, buf, tid);
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
-    double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
@@ -205,6 +173,58 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
         out[r * WAVE + lane] = wave_masking_row(L, nm, T, lane, r);
     }
+}
+
+// One workgroup per (block, variant pair) -- {0,1} = L/R, {2,3} = M/S,
+// {4,5} = M/S without the drop (MLD) -- runs the pair's variants one after the
+// other: a third of the dispatches and row-mask passes of one workgroup per
+// variant, and the two M/S variants of a pair read the same spectrum
+// neighbourhoods.  Written as two straight-line calls, not a loop: a loop
+// over the variants keeps ~80 more VGPRs live (loop-invariant addresses).
+__global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
+                                                         PacMasterChunkBuf K, PacMasterFields F,
+                                                         PacMasterChunk ck) {
+    __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
+    __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // masker lists (region B)
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int64_t item = xcd_item(blockIdx.x, gridDim.x);
+    const int npair = ck.nch == 2 ? 3 : 1;     // mono master: BTHR_L only
+    const int64_t j = item / npair;            // block within the chunk
+    const int vb = 2 * (int)(item % npair);
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, j, &cp)) return;     // uniform per workgroup
+    const int64_t gb = cp.gb;
+    const int fl = F.bsf ? F.bsf[gb] : 0;
+    if (fl & PAC_BS_SHORT) return;                          // k_master_thr_short's
+    // rows whose lines' bands use the pair: L/R (v < 2) where LRMS = 0, the
+    // M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
+    // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
+    int& rowmask = reinterpret_cast<int*>(tmp)[0];          // region B is idle until the lists
+    if (tid == 0) rowmask = 0;
+    __syncthreads();
+    {
+        const int want = vb >= 2 ? 1 : 0;
+        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+        int bits = 0;
+#pragma unroll
+        for (int i = 0; i < PAC_HALFN / FRONT_NT; ++i) {
+            const int l = i * FRONT_NT + tid;
+            if (l < lend && F.lrms[gb * PAC_NB + T->band_of_line[l]] == want) bits |= 1 << (l / WAVE);
+        }
+        bits = __builtin_amdgcn_readfirstlane(wave_or_i(bits));
+        if (lane == 0 && bits) atomicOr(&rowmask, bits);
+    }
+    __syncthreads();
+    const int rows = __builtin_amdgcn_readfirstlane(rowmask);   // wave-uniform: the branches below are
+    if (!rows) return;
+    const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
+    thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid);
+    if (ck.nch != 2) return;
+    __syncthreads();                                        // the first variant's lists are read
+    int t2 = tid;                // opaque copy: no per-lane address of the first call is kept live for the second
+    asm volatile("" : "+v"(t2));
+    thr_variant(T, spec, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2);
 }
 
 // Block-switching extension (pac_bs.h): the thresholds of a SHORT frame.  One

@@ -124,6 +124,23 @@ __device__ __forceinline__ void grp_fft(double2* buf, const double2* __restrict_
     grp_sync<NT>();
 }
 
+// Bank-conflict-free LDS layout of the Stockham stage buffers.  MI355X LDS
+// banking: ds_read_b128 serves 16-lane groups over a 256-B bank row,
+// ds_write_b128 8-lane groups over 128 B, so the stride-4 and stride-16
+// writes of the first stages cost 4-way / 2-way conflicts in the plain
+// layout.  Element i of an intermediate stage buffer is stored at
+// i ^ fft_swz(i), fft_swz a GF(2)-linear function of index bits 3..7 (found
+// by exhaustive search over the stages' access patterns, N = 128..1024): every
+// read and write of every stage is conflict-free (2/3 of the plain layout's
+// LDS cycles).  The first stage reads and the last stage writes the plain
+// layout, so callers never see it.  Linear: fft_swz(a + b) =
+// fft_swz(a) ^ fft_swz(b) for bit-disjoint a, b (one swizzle per butterfly,
+// the other offsets are compile-time constants).
+__host__ __device__ constexpr int fft_swz(int i) {
+    return (((i >> 3) & 1) * 1) ^ (((i >> 4) & 1) * 14) ^ (((i >> 5) & 1) * 2) ^ (((i >> 6) & 1) * 1) ^
+           (((i >> 7) & 1) * 7);
+}
+
 // Self-sorting (Stockham) FFT of n = 2^LOG complex values in natural order,
 // radix-4 stages (+ one radix-2 stage for odd LOG), ping-ponging between src
 // and dst; every read is unit-stride across lanes and no bit-reversal
@@ -143,7 +160,11 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
             const int j = j0 + tid;
             if (N4 % NT != 0 && j >= N4) break;
             const int k = j & (Ns - 1);
-            double2 v0 = src[j], v1 = src[j + N4], v2 = src[j + 2 * N4], v3 = src[j + 3 * N4];
+            const bool swi = st > 0, swo = st + 1 < LOG / 2 || (LOG & 1);   // plain in first, out last
+            const int xj = swi ? fft_swz(j) : 0;
+            double2 v0 = src[j ^ xj], v1 = src[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
+            double2 v2 = src[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
+            double2 v3 = src[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
             if (Ns > 1) {
                 const int e = k * (256 / Ns);           // angle -2 pi k r / (4 Ns)
                 v1 = cmul(v1, tw[e]);
@@ -155,10 +176,11 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
             const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
             const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);   // -i (v1 - v3)
             const int o = ((j - k) << 2) + k;
-            dst[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
-            dst[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
-            dst[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
-            dst[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+            const int xo = swo ? fft_swz(o) : 0;
+            dst[o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
+            dst[(o + Ns) ^ xo ^ (swo ? fft_swz(Ns) : 0)] = make_double2(a1.x + a3.x, a1.y + a3.y);
+            dst[(o + 2 * Ns) ^ xo ^ (swo ? fft_swz(2 * Ns) : 0)] = make_double2(a0.x - a2.x, a0.y - a2.y);
+            dst[(o + 3 * Ns) ^ xo ^ (swo ? fft_swz(3 * Ns) : 0)] = make_double2(a1.x - a3.x, a1.y - a3.y);
         }
         double2* t = src; src = dst; dst = t;
     }
@@ -168,8 +190,9 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
         for (int j0 = 0; j0 < N / 2; j0 += NT) {
             const int j = j0 + tid;
             if ((N / 2) % NT != 0 && j >= N / 2) break;
-            const double2 v0 = src[j];
-            const double2 v1 = cmul(src[j + N / 2], tw[j * (1024 / N)]);
+            const int xj = fft_swz(j);
+            const double2 v0 = src[j ^ xj];
+            const double2 v1 = cmul(src[(j + N / 2) ^ xj ^ fft_swz(N / 2)], tw[j * (1024 / N)]);
             dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
             dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
         }
@@ -199,10 +222,12 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
             const int j = q * NT + tid;
             if (N4 < NT && j >= N4) break;
             const int k = j & (Ns - 1);
-            v[q][0] = buf[j];
-            v[q][1] = buf[j + N4];
-            v[q][2] = buf[j + 2 * N4];
-            v[q][3] = buf[j + 3 * N4];
+            const bool swi = st > 0;
+            const int xj = swi ? fft_swz(j) : 0;
+            v[q][0] = buf[j ^ xj];
+            v[q][1] = buf[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
+            v[q][2] = buf[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
+            v[q][3] = buf[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
             if (Ns > 1) {
                 const int e = k * (256 / Ns);
                 v[q][1] = cmul(v[q][1], tw[e]);
@@ -221,10 +246,12 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
             const double2 a2 = make_double2(v[q][1].x + v[q][3].x, v[q][1].y + v[q][3].y);
             const double2 a3 = make_double2(v[q][1].y - v[q][3].y, v[q][3].x - v[q][1].x);
             const int o = ((j - k) << 2) + k;
-            buf[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
-            buf[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
-            buf[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
-            buf[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+            const bool swo = st + 1 < LOG / 2 || (LOG & 1);
+            const int xo = swo ? fft_swz(o) : 0;
+            buf[o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
+            buf[(o + Ns) ^ xo ^ (swo ? fft_swz(Ns) : 0)] = make_double2(a1.x + a3.x, a1.y + a3.y);
+            buf[(o + 2 * Ns) ^ xo ^ (swo ? fft_swz(2 * Ns) : 0)] = make_double2(a0.x - a2.x, a0.y - a2.y);
+            buf[(o + 3 * Ns) ^ xo ^ (swo ? fft_swz(3 * Ns) : 0)] = make_double2(a1.x - a3.x, a1.y - a3.y);
         }
     }
     if (LOG & 1) {
@@ -235,8 +262,9 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
         for (int q = 0; q < J2; ++q) {
             const int j = q * NT + tid;
             if ((N / 2) < NT && j >= N / 2) break;
-            v0[q] = buf[j];
-            v1[q] = cmul(buf[j + N / 2], tw[j * (1024 / N)]);
+            const int xj = fft_swz(j);
+            v0[q] = buf[j ^ xj];
+            v1[q] = cmul(buf[(j + N / 2) ^ xj ^ fft_swz(N / 2)], tw[j * (1024 / N)]);
         }
         grp_sync<NT>();
 #pragma unroll
@@ -272,10 +300,12 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
             for (int q = 0; q < J; ++q) {
                 const int j = q * NT + tid;
                 const int k = j & (Ns - 1);
-                v[u][q][0] = bufs[u][j];
-                v[u][q][1] = bufs[u][j + N4];
-                v[u][q][2] = bufs[u][j + 2 * N4];
-                v[u][q][3] = bufs[u][j + 3 * N4];
+                const bool swi = st > 0;
+                const int xj = swi ? fft_swz(j) : 0;
+                v[u][q][0] = bufs[u][j ^ xj];
+                v[u][q][1] = bufs[u][(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
+                v[u][q][2] = bufs[u][(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
+                v[u][q][3] = bufs[u][(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
                 if (Ns > 1) {
                     const int e = k * (256 / Ns);
                     v[u][q][1] = cmul(v[u][q][1], tw[e]);
@@ -296,10 +326,12 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
                 const double2 a2 = make_double2(w[1].x + w[3].x, w[1].y + w[3].y);
                 const double2 a3 = make_double2(w[1].y - w[3].y, w[3].x - w[1].x);
                 const int o = ((j - k) << 2) + k;
-                bufs[u][o] = make_double2(a0.x + a2.x, a0.y + a2.y);
-                bufs[u][o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
-                bufs[u][o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
-                bufs[u][o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+                const bool swo = st + 1 < LOG / 2;      // LOG even here
+                const int xo = swo ? fft_swz(o) : 0;
+                bufs[u][o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
+                bufs[u][(o + Ns) ^ xo ^ (swo ? fft_swz(Ns) : 0)] = make_double2(a1.x + a3.x, a1.y + a3.y);
+                bufs[u][(o + 2 * Ns) ^ xo ^ (swo ? fft_swz(2 * Ns) : 0)] = make_double2(a0.x - a2.x, a0.y - a2.y);
+                bufs[u][(o + 3 * Ns) ^ xo ^ (swo ? fft_swz(3 * Ns) : 0)] = make_double2(a1.x - a3.x, a1.y - a3.y);
             }
     }
     grp_sync<NT>();
@@ -328,7 +360,11 @@ __device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, do
                 const int j = j0 + tid;
                 if (N4 % NT != 0 && j >= N4) break;
                 const int k = j & (Ns - 1);
-                double2 v0 = src[j], v1 = src[j + N4], v2 = src[j + 2 * N4], v3 = src[j + 3 * N4];
+                const bool swi = st > 0, swo = st + 1 < LOG / 2 || (LOG & 1);
+                const int xj = swi ? fft_swz(j) : 0;
+                double2 v0 = src[j ^ xj], v1 = src[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
+                double2 v2 = src[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
+                double2 v3 = src[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
                 if (Ns > 1) {
                     const int e = k * (256 / Ns);
                     v1 = cmul(v1, tw[e]);
@@ -340,10 +376,11 @@ __device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, do
                 const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
                 const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);
                 const int o = ((j - k) << 2) + k;
-                dst[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
-                dst[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
-                dst[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
-                dst[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+                const int xo = swo ? fft_swz(o) : 0;
+                dst[o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
+                dst[(o + Ns) ^ xo ^ (swo ? fft_swz(Ns) : 0)] = make_double2(a1.x + a3.x, a1.y + a3.y);
+                dst[(o + 2 * Ns) ^ xo ^ (swo ? fft_swz(2 * Ns) : 0)] = make_double2(a0.x - a2.x, a0.y - a2.y);
+                dst[(o + 3 * Ns) ^ xo ^ (swo ? fft_swz(3 * Ns) : 0)] = make_double2(a1.x - a3.x, a1.y - a3.y);
             }
         }
         double2* t = sa; sa = da; da = t;
@@ -359,8 +396,9 @@ __device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, do
             for (int j0 = 0; j0 < N / 2; j0 += NT) {
                 const int j = j0 + tid;
                 if ((N / 2) % NT != 0 && j >= N / 2) break;
-                const double2 v0 = src[j];
-                const double2 v1 = cmul(src[j + N / 2], tw[j * (1024 / N)]);
+                const int xj = fft_swz(j);
+                const double2 v0 = src[j ^ xj];
+                const double2 v1 = cmul(src[(j + N / 2) ^ xj ^ fft_swz(N / 2)], tw[j * (1024 / N)]);
                 dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
                 dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
             }

@@ -318,6 +318,7 @@ struct pac_ctx {
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
     DevBuf<double2> m_spec;               // [chunk][2][PAC_SPEC_LD] k_master_spec -> k_master_thr
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
+    DevBuf<uint32_t> m_rowm;                // [nblocks] k_master_lrms -> k_master_thr row masks
     DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack)
     DevBuf<int64_t> st_extra, st_deposit;
     DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
@@ -395,7 +396,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
-    c->m_lrms.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
+    c->m_lrms.release(); c->m_rowm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
@@ -770,7 +771,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         cbmax = std::max<int64_t>(cbmax, (int64_t)n_s * S);
         g0 = g1;
     }
-    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
+    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
@@ -779,7 +780,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         return rc;
     if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
-                      nullptr, nullptr, nullptr, c->m_codes.p, nullptr};
+                      nullptr, nullptr, nullptr, c->m_codes.p, nullptr, c->m_rowm.p};
     if (p->block_switch) {     // pac_bs.h: attack flags, then each block's PAC_BS_* flags
         if ((rc = c->bs_att.ensure(nblocks + 1)) || (rc = c->bs_fl.ensure(nblocks + 1))) return rc;
         hipLaunchKernelGGL(k_bs_attack, dim3((unsigned)((nblocks + 1) / 2)), dim3(64), 0, c->stream, src, nblocks,

@@ -52,6 +52,7 @@ struct PacMasterFields {
     uint8_t* dbg_len;    // [G][1024]
     uint16_t* codes;     // [G][1024] signed mantissa codes (tail -> pack; 0 where ba == 0)
     const uint8_t* bsf;  // [nblocks] PAC_BS_* flags (block-switching extension), or null: off
+    uint32_t* rowm;      // [nblocks] 64-line rows of L/R-coded bands (bits 0-15), M/S-coded (16-31), k_master_lrms
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of streams
@@ -187,7 +188,6 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
     __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // masker lists (region B)
     const int tid = threadIdx.x;
-    const int lane = tid & (WAVE - 1);
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
     const int npair = ck.nch == 2 ? 3 : 1;     // mono master: BTHR_L only
     const int64_t j = item / npair;            // block within the chunk
@@ -199,24 +199,16 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     if (fl & PAC_BS_SHORT) return;                          // k_master_thr_short's
     // rows whose lines' bands use the pair: L/R (v < 2) where LRMS = 0, the
     // M/S thresholds (v >= 2) where LRMS = 1 (getStereoMaskThreshold takes
-    // each band's SMR from one mode, psychoac.py:662-682); none: nothing to do
-    int& rowmask = reinterpret_cast<int*>(tmp)[0];          // region B is idle until the lists
-    if (tid == 0) rowmask = 0;
-    __syncthreads();
-    {
-        const int want = vb >= 2 ? 1 : 0;
-        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-        int bits = 0;
-#pragma unroll
-        for (int i = 0; i < PAC_HALFN / FRONT_NT; ++i) {
-            const int l = i * FRONT_NT + tid;
-            if (l < lend && F.lrms[gb * PAC_NB + T->band_of_line[l]] == want) bits |= 1 << (l / WAVE);
-        }
-        bits = __builtin_amdgcn_readfirstlane(wave_or_i(bits));
-        if (lane == 0 && bits) atomicOr(&rowmask, bits);
+    // each band's SMR from one mode, psychoac.py:662-682; k_master_lrms
+    // records both masks); none: nothing to do.  Mono: every row of a band.
+    int rows;
+    if (ck.nch == 2) {
+        const uint32_t rm = F.rowm[gb];
+        rows = (int)(vb >= 2 ? rm >> 16 : rm & 0xffffu);
+    } else {
+        rows = (2 << ((T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1] - 1) / WAVE)) - 1;
     }
-    __syncthreads();
-    const int rows = __builtin_amdgcn_readfirstlane(rowmask);   // wave-uniform: the branches below are
+    rows = __builtin_amdgcn_readfirstlane(rows);
     if (!rows) return;
     const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
     thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid);
@@ -529,12 +521,22 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     double2* leafv1 = bufA + 64;
     if (has && sub == 0) { leafv0[lf] = lv0; leafv1[lf] = lv1; }
     __syncthreads();
-    if (tid < PAC_NB) {
-        int i0 = T->lr_first_leaf[tid], i1 = i0;
-        const int n = 2 * T->nlines[tid];
-        const double2 sd = np_csum_combine<5>(leafv0, i0, n);
-        const double2 ss = np_csum_combine<5>(leafv1, i1, n);
-        F.lrms[gb * PAC_NB + tid] = (uint8_t)(hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0);
+    if (tid < WAVE) {                              // wave 0: the decisions and the rows they select
+        int rows = 0;
+        if (tid < PAC_NB) {
+            int i0 = T->lr_first_leaf[tid], i1 = i0;
+            const int nl = T->nlines[tid];
+            const double2 sd = np_csum_combine<5>(leafv0, i0, 2 * nl);
+            const double2 ss = np_csum_combine<5>(leafv1, i1, 2 * nl);
+            const int ms = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
+            F.lrms[gb * PAC_NB + tid] = (uint8_t)ms;
+            if (nl) {                              // the 64-line rows of the band's lines
+                const int r0 = T->lower[tid] / WAVE, r1 = (T->lower[tid] + nl - 1) / WAVE;
+                rows = ((2 << r1) - (1 << r0)) << (ms ? 16 : 0);
+            }
+        }
+        rows = wave_or_i(rows);
+        if (tid == 0) F.rowm[gb] = (uint32_t)rows;
     }
 }
 

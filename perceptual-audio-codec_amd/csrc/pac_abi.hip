@@ -223,6 +223,9 @@ static void build_tables(int fs, int window, PacTables* t) {
             const long double e = kl * (long double)t->bark_line[l];
             t->pow_kl[l] = (double)exp2l(e);
             t->pow_mkl[l] = (double)exp2l(-e);
+            const long double zb = (long double)t->bark_bin[l];
+            t->pow_pl[l] = (double)exp2l(kl * (zb - 0.5L));
+            t->pow_pu[l] = (double)exp2l(-kl * (zb + 0.5L));
         }
     }
     {   // block-switching extension tables (pac_bs.h), the same formulas at N = 512

@@ -41,7 +41,7 @@ __device__ __forceinline__ double bs_long_win(const PacTables* __restrict__ T, i
 //   X[k] = sc * sum_j v(j) cos(pi/256 (j + 1/2)(k + 1/2)),
 // via the 128-point Stockham FFT (the 1024-line grp_dct4 at M = 256).
 // scr: 256 double2 of LDS private to the wave; out(k, X[k]) receives the lines.
-template <class V, class OUT>
+template <bool SWZ = true, class V, class OUT>
 __device__ __forceinline__ void wave_dct4_256(const V& v, const PacTables* __restrict__ T, double2* scr, int lane,
                                               double sc, const OUT& out) {
 #pragma unroll
@@ -49,7 +49,7 @@ __device__ __forceinline__ void wave_dct4_256(const V& v, const PacTables* __res
         const int q = q0 + lane;
         scr[q] = cmul(make_double2(v(2 * q), v(255 - 2 * q)), T->mdct_pre_s[q]);
     }
-    const double2* Y = grp_fft_stockham<7, WAVE>(scr, scr + 128, T->fft_tw, lane);
+    const double2* Y = grp_fft_stockham<7, WAVE, SWZ>(scr, scr + 128, T->fft_tw, lane);
 #pragma unroll
     for (int q0 = 0; q0 < 128; q0 += WAVE) {
         const int q = q0 + lane;

@@ -56,6 +56,9 @@ struct PacTables {
     // factored masking sums (pac_wave.h): 2^(KL z_l) and 2^(-KL z_l) per line,
     // KL = -27 log2(10)/10 as the device rounds it, evaluated in long double
     double pow_kl[PAC_HALFN], pow_mkl[PAC_HALFN];
+    // the masker lists' factored terms per FFT bin k (grp_find_maskers):
+    // 2^(KL (z_k - 1/2)) and 2^(-KL (z_k + 1/2)), z_k = Bark(k fs//N), long double
+    double pow_pl[PAC_HALFN], pow_pu[PAC_HALFN];
     // block-switching extension (pac_bs.h): the short transform (N = 512,
     // 256 lines), its window, and the masking model's tables at N = 512
     double sine_s[512];               // short MDCT window (sine, or KBD alpha 4)

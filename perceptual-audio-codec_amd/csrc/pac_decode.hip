@@ -248,7 +248,7 @@ __device__ __forceinline__ double imdct_window_at(const double* U, const PacTabl
 // register budget
 __device__ __forceinline__ void dec_short_imdct(double* Lc, const PacTables* __restrict__ T, double2* buf, int tid) {
     const int k = tid / WAVE;
-    wave_dct4_256([&](int j) { return Lc[4 * j + k]; }, T, buf + 256 * k, tid & (WAVE - 1), 2.0,
+    wave_dct4_256<false>([&](int j) { return Lc[4 * j + k]; }, T, buf + 256 * k, tid & (WAVE - 1), 2.0,
                   [&](int j, double v) { Lc[4 * j + k] = v; });
 }
 
@@ -336,7 +336,8 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
                 __syncthreads();
                 U = lines[c];
             } else {
-                U = grp_dct4<256>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
+                // plain FFT layout: the swizzle's index math would cost this kernel a wave per SIMD
+                U = grp_dct4<256, false>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
             }
             const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
             auto emit = [&](int i, double w0, double w1) {

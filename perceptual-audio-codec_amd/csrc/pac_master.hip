@@ -5,21 +5,26 @@
 // Pass 1 sweeps time slices (chunk = blocks t0..t0+S-1 of every stream of a
 // stream group, PacMasterChunk) so the serial reservoir chain of every stream
 // advances in parallel; pass 2 packs every channel-block at its final offset:
-//   k_master_thr    one workgroup per (block, variant): the six calcBTHR()
-//                   calls of getStereoMaskThreshold (psychoac.py:540-562) incl.
-//                   the in-place Hann chains -> chunk thr[j][v][1024]
-//   k_master_front  one workgroup per block: LRMS decision (codec.py:94-102),
-//                   MDCT L/R + overall scale (codec.py:237-246), M/S lines, MLD
-//                   combination and per-band SMR selection (psychoac.py:533-682)
-//   k_master_tail   one wave per STREAM of the chunk, its blocks in order:
+//   k_master_lrms   one workgroup per block: LRMS decision (codec.py:94-102)
+//                   and the 64-line rows each coding mode's bands use
+//   k_master_spec   one workgroup per block: FFT(a), FFT(b) of the windowed
+//                   channels (the first in-place chains of calcBTHR)
+//   k_master_thr    one workgroup per (block, variant pair): the six calcBTHR()
+//                   calls of getStereoMaskThreshold (psychoac.py:540-562), each
+//                   variant's spectrum derived from FFT(a), FFT(b) (M/S and the
+//                   in-place Hann multiplies in the frequency domain) -> chunk
+//                   thr[j][v][1024], only the rows the variant's bands use
+//   k_master_front  one workgroup per block: MDCT L/R + overall scale
+//                   (codec.py:237-246), M/S lines, MLD combination and per-band
+//                   SMR selection (psychoac.py:533-682)
+//   k_master_tail   16 lanes per STREAM of the chunk, its blocks in order:
 //                   withdrawBits, the two BitAlloc calls with the extraBits carry
 //                   (codec.py:222-260, bitalloc.py:129-184), scale factors,
-//                   10-table Huffman length scoring, depositBits (codec.py:111-124)
-//                   and the channel-block's byte count
+//                   mantissas, 10-table Huffman length scoring, depositBits
+//                   (codec.py:111-124) and the channel-block's byte count
 //   (k_scan_* over the byte counts -> final offsets, as the origin profile)
-//   k_master_pack   one workgroup per block (pass 2): MDCT L/R recomputed from
-//                   the PCM (cheaper than keeping 16 KB of lines per block in
-//                   HBM), M/S lines, sign bits, Huffman codes and LRMS packed
+//   k_master_pack   one workgroup per block (pass 2): from the tail's stored
+//                   mantissa codes, sign bits, Huffman codes and LRMS packed
 //                   MSB-first (pacfile.py:288-351) straight to the final offset.
 // The tail of chunk i runs on a second HIP stream, concurrently with the
 // threshold/front kernels of chunk i+1 (double-buffered chunk outputs).
@@ -33,9 +38,9 @@ struct PacMasterChunkBuf {
     double* lines;      // [Bc][2][1024]  LRMSmdctLines
     double* smr;        // [Bc][2][25]
     double* bandpeak;   // [Bc][2][25]    max |line| per band
-    double2* spec;      // [Bc][2][PAC_SPEC_LD] FFT bins 0..1024 of a and b (k_master_spec)
+    double2* spec;      // [Bc][2][PAC_SPEC_LD] FFT bins -2..1026 of a and b (k_master_spec)
 };
-#define PAC_SPEC_LD 1040    // double2 per spectrum: bins 0..1024, padded to 256 B
+#define PAC_SPEC_LD 1040    // double2 per spectrum: bins -2..1026 at [bin + 2], padded to 256 B
 
 // per-call fields; channel-block g = nch gb + ch (gb = global block, file order)
 struct PacMasterFields {
@@ -108,27 +113,23 @@ __device__ __forceinline__ double variant_sample(const BlockPcm& rL, const Block
 // FFT's own order (bins within ~1e-16 of the spectrum's maximum).
 #define PAC_HANN_C 0.9999988234517019      // cos(pi / 2048)
 #define PAC_HANN_S 0.0015339801862847655   // sin(pi / 2048)
-__device__ __forceinline__ double2 spec_at(const double2* __restrict__ S, int k) {
-    const int kk = k < 0 ? -k : (k > 1024 ? 2048 - k : k);
-    double2 x = S[kk];
-    if (kk != k) x.y = -x.y;
-    return x;
-}
 __device__ __forceinline__ double2 hann_tap(double2 xm, double2 x0, double2 xp) {
-    const double mr = PAC_HANN_C * xm.x - PAC_HANN_S * xm.y, mi = PAC_HANN_C * xm.y + PAC_HANN_S * xm.x;
-    const double pr = PAC_HANN_C * xp.x + PAC_HANN_S * xp.y, pi = PAC_HANN_C * xp.y - PAC_HANN_S * xp.x;
-    return make_double2(0.5 * x0.x - 0.25 * (mr + pr), 0.5 * x0.y - 0.25 * (mi + pi));
+    // e^{i pi/N} xm + e^{-i pi/N} xp, then x0/2 - that/4
+    const double sx = xm.x + xp.x, dy = xm.y - xp.y, sy = xm.y + xp.y, dx = xm.x - xp.x;
+    const double re = __builtin_fma(PAC_HANN_C, sx, -(PAC_HANN_S * dy));
+    const double im = __builtin_fma(PAC_HANN_C, sy, PAC_HANN_S * dx);
+    return make_double2(__builtin_fma(-0.25, re, 0.5 * x0.x), __builtin_fma(-0.25, im, 0.5 * x0.y));
 }
-// buf[k].x = |V_v[k]|^2, k < 1024; S = the block's spectra (A at S, B at
-// S + PAC_SPEC_LD).  Each thread owns 4 consecutive bins (8 loads of the
-// neighbourhood instead of 5 per bin).
+// buf[k].x = |V_v[k]|^2, k < 1024; S = the block's spectra (bin k of A at
+// S[k + 2], of B at S[PAC_SPEC_LD + k + 2], k = -2..1026).  Each thread owns 4
+// consecutive bins (8 loads of the neighbourhood instead of 5 per bin).
 template <int NT>
 __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, int v, double2* buf, int tid) {
     static_assert(NT * 4 == 1024, "4 bins per thread");
     const int k0 = 4 * tid;
     double2 X[4];
     if (v < 2) {
-        const double2* P = S + (v ? PAC_SPEC_LD : 0) + k0;
+        const double2* P = S + (v ? PAC_SPEC_LD : 0) + 2 + k0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) X[i] = P[i];
     } else {
@@ -136,7 +137,7 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
         double2 m[8];                                // bins k0 - 2 .. k0 + 5
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const double2 a = spec_at(S, k0 - 2 + i), b = spec_at(S + PAC_SPEC_LD, k0 - 2 + i);
+            const double2 a = S[k0 + i], b = S[PAC_SPEC_LD + k0 + i];
             m[i] = make_double2(0.5 * (a.x + sg * b.x), 0.5 * (a.y + sg * b.y));
         }
         double2 h[6];                                // M h at bins k0 - 1 .. k0 + 4
@@ -574,15 +575,22 @@ __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTab
                                 variant_sample(rL, rR, T, 1, 2 * n, fl), variant_sample(rL, rR, T, 1, 2 * n + 1, fl));
         }, T, bufA, bufB, tid, nyq);
     }
-    double2* o = K.spec + j * 2 * PAC_SPEC_LD;
+    // bins -2..1026 at o[bin + 2]: the mirrored edge bins X[-k] = X[2048-k] =
+    // conj X[k] stored, so the taps of k_master_thr need no index arithmetic
+    double2* o = K.spec + j * 2 * PAC_SPEC_LD + 2;
 #pragma unroll
     for (int k = tid; k < 1024; k += 256) {
         o[k] = bufA[k];
         o[PAC_SPEC_LD + k] = bufB[k];
     }
-    if (tid == 0) {
-        o[1024] = make_double2(nyq[0], 0.0);
-        o[PAC_SPEC_LD + 1024] = make_double2(nyq[1], 0.0);
+    if (tid < 2) {                                 // bins 1024 (Nyquist, real) and -1 .. -2
+        o[tid * PAC_SPEC_LD + 1024] = make_double2(nyq[tid], 0.0);
+        const double2 a1 = (tid ? bufB : bufA)[1], a2 = (tid ? bufB : bufA)[2];
+        o[tid * PAC_SPEC_LD - 1] = make_double2(a1.x, -a1.y);
+        o[tid * PAC_SPEC_LD - 2] = make_double2(a2.x, -a2.y);
+        const double2 b1 = (tid ? bufB : bufA)[1023], b2 = (tid ? bufB : bufA)[1022];
+        o[tid * PAC_SPEC_LD + 1025] = make_double2(b1.x, -b1.y);
+        o[tid * PAC_SPEC_LD + 1026] = make_double2(b2.x, -b2.y);
     }
 }
 

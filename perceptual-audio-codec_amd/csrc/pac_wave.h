@@ -146,7 +146,7 @@ __host__ __device__ constexpr int fft_swz(int i) {
 // and dst; every read is unit-stride across lanes and no bit-reversal
 // permutation is needed.  Returns the buffer holding the result (always dst:
 // LOG = 10 has 5 stages, LOG = 9 has 4 + 1).  tw[k] = exp(-2 pi i k / 1024).
-template <int LOG, int NT>
+template <int LOG, int NT, bool SWZ = true>   // SWZ = false: plain layout (fewer VGPRs, bit-identical)
 __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
                                                      const double2* __restrict__ tw, int tid) {
     constexpr int N = 1 << LOG;
@@ -160,7 +160,7 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
             const int j = j0 + tid;
             if (N4 % NT != 0 && j >= N4) break;
             const int k = j & (Ns - 1);
-            const bool swi = st > 0, swo = st + 1 < LOG / 2 || (LOG & 1);   // plain in first, out last
+            const bool swi = SWZ && st > 0, swo = SWZ && (st + 1 < LOG / 2 || (LOG & 1));   // plain in first, out last
             const int xj = swi ? fft_swz(j) : 0;
             double2 v0 = src[j ^ xj], v1 = src[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
             double2 v2 = src[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
@@ -190,9 +190,9 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
         for (int j0 = 0; j0 < N / 2; j0 += NT) {
             const int j = j0 + tid;
             if ((N / 2) % NT != 0 && j >= N / 2) break;
-            const int xj = fft_swz(j);
+            const int xj = SWZ ? fft_swz(j) : 0;
             const double2 v0 = src[j ^ xj];
-            const double2 v1 = cmul(src[(j + N / 2) ^ xj ^ fft_swz(N / 2)], tw[j * (1024 / N)]);
+            const double2 v1 = cmul(src[(j + N / 2) ^ xj ^ (SWZ ? fft_swz(N / 2) : 0)], tw[j * (1024 / N)]);
             dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
             dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
         }
@@ -416,7 +416,7 @@ __device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, do
 // via the 512-point complex Stockham FFT (even/odd interleave, pre- and
 // post-twiddles).  buf: 1024 double2 of LDS; X = (double*)buf on return (first
 // 8 KB), the second 8 KB is free scratch.
-template <int NT, class V>
+template <int NT, bool SWZ = true, class V>
 __device__ __forceinline__ double* grp_dct4(const V& v, const PacTables* __restrict__ T, double2* buf, int tid,
                                             double sc) {
 #pragma unroll
@@ -424,7 +424,7 @@ __device__ __forceinline__ double* grp_dct4(const V& v, const PacTables* __restr
         const int q = q0 + tid;
         buf[q] = cmul(make_double2(v(2 * q), v(1023 - 2 * q)), T->mdct_pre[q]);
     }
-    const double2* Y = grp_fft_stockham<9, NT>(buf, buf + 512, T->fft_tw, tid);   // = buf + 512
+    const double2* Y = grp_fft_stockham<9, NT, SWZ>(buf, buf + 512, T->fft_tw, tid);   // = buf + 512
     double* X = reinterpret_cast<double*>(buf);
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
@@ -838,13 +838,8 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
             rz[q] = T->bark_bin[k];
             rku[q] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
             rE[q] = pac_exp2(rB[q]);
-            double h, lo;
-            dd_affine(rB[q], PAC_KL, rz[q], 0.5, h, lo);       // B + KL (z - 1/2)
-            rPL[q] = pac_exp2_dd(h, lo);
-            if (!loud) {
-                dd_affine(rB[q], PAC_KL, -0.5, rz[q], h, lo);  // B - KL (z + 1/2)
-                rPU[q] = pac_exp2_dd(h, lo);
-            }
+            rPL[q] = rE[q] * T->pow_pl[k];                 // 2^(B + KL (z - 1/2))
+            if (!loud) rPU[q] = rE[q] * T->pow_pu[k];      // 2^(B - KL (z + 1/2))
         }
         lb[q] = __ballot(loud);
         if (lane == 0) cnt2[q * NW + w] = __popcll(lb[q]);

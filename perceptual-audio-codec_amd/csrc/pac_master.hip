@@ -408,7 +408,7 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 template <int NT, bool NYQ = false, class D4>
 __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
                                                     double2* bufA, double2* bufB, int tid,
-                                                    double* nyq = nullptr) {
+                                                    double* nyq = nullptr) {   // nyq: thread 0's
 #pragma unroll 4
     for (int n0 = 0; n0 < 1024; n0 += NT) {
         const int n = n0 + tid;
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
 __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTables* __restrict__ T,
                                                      PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
-    __shared__ double nyq[2];
+    double nyq[2] = {0.0, 0.0};   // thread 0's registers (the split's pair p = 0): 32 KB LDS, 5 WG/CU
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     ChunkPos cp;
@@ -583,14 +583,17 @@ __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTab
         o[k] = bufA[k];
         o[PAC_SPEC_LD + k] = bufB[k];
     }
-    if (tid < 2) {                                 // bins 1024 (Nyquist, real) and -1 .. -2
-        o[tid * PAC_SPEC_LD + 1024] = make_double2(nyq[tid], 0.0);
-        const double2 a1 = (tid ? bufB : bufA)[1], a2 = (tid ? bufB : bufA)[2];
-        o[tid * PAC_SPEC_LD - 1] = make_double2(a1.x, -a1.y);
-        o[tid * PAC_SPEC_LD - 2] = make_double2(a2.x, -a2.y);
-        const double2 b1 = (tid ? bufB : bufA)[1023], b2 = (tid ? bufB : bufA)[1022];
-        o[tid * PAC_SPEC_LD + 1025] = make_double2(b1.x, -b1.y);
-        o[tid * PAC_SPEC_LD + 1026] = make_double2(b2.x, -b2.y);
+    if (tid == 0) {                                // bins 1024 (Nyquist, real), -1, -2, 1025, 1026
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const double2* X = u ? bufB : bufA;
+            double2* q = o + u * PAC_SPEC_LD;
+            q[1024] = make_double2(nyq[u], 0.0);
+            q[-1] = make_double2(X[1].x, -X[1].y);
+            q[-2] = make_double2(X[2].x, -X[2].y);
+            q[1025] = make_double2(X[1023].x, -X[1023].y);
+            q[1026] = make_double2(X[1022].x, -X[1022].y);
+        }
     }
 }
 

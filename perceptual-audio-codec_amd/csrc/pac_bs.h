@@ -248,7 +248,7 @@ __device__ __forceinline__ void wave_threshold_short(char* R, const PacTables* _
         const double lower = (V < nm ? LP[V] : 0.0) * T->pow_mkl_s[l];
         const double upq = LQ[U] * T->pow_kl_s[l];
         const int Ul = U < nm ? lpre[U] : nloud;
-        const int umax = wave_max_i(Ul);
+        const int umax = __builtin_amdgcn_readlane(Ul, WAVE - 1);   // U nondecreasing in l (zl ascending)
         double up = 0.0;
         for (int j = 0; j < umax; ++j) {
             const double t = pac_exp2(__builtin_fma(__dsub_rn(zl, lz[j]) - 0.5, lku[j], lB[j]));

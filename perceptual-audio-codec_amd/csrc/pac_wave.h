@@ -892,6 +892,58 @@ __device__ __forceinline__ int wave_or_i(int v) {
 __device__ __forceinline__ int wave_min_i(int v) { return wave_ext_i<false>(v); }
 __device__ __forceinline__ int wave_max_i(int v) { return wave_ext_i<true>(v); }
 
+// v_min_f64 / v_max_f64 without the canonicalising v_max_f64 x, x the compiler
+// adds around fmin/fmax in IEEE mode (the operands are never NaN)
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// Wave extremum read from lane 0: four full-row DPP steps (bound_ctrl, every
+// lane has a source), then rows 0|1 and 2|3 by v_permlane16_swap and the
+// halves by v_permlane32_swap -- 3 VALU per step instead of the
+// compare-select and row_bcast copies of wave_ext_f64.
+template <bool MAX>
+__device__ __forceinline__ double wave_ext0_f64(double v) {
+    auto f = [](double a, double b) { return MAX ? vmax_f64(a, b) : vmin_f64(a, b); };
+    v = f(v, dpp_full_f64<PAC_DPP_QXOR1>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_QXOR2>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_HMIRROR>(v));
+    v = f(v, dpp_full_f64<PAC_DPP_MIRROR>(v));
+    {
+        const long long b = __double_as_longlong(v);
+        const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+        v = f(__longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]),
+              __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]));
+    }
+    {
+        const long long b = __double_as_longlong(v);
+        const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+        v = f(__longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]),
+              __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]));
+    }
+    return readlane_f64(v, 0);
+}
+// integer minimum, the same shape (DPP steps fold into v_min_i32_dpp)
+__device__ __forceinline__ int wave_min0_i(int v) {
+    v = min(v, __builtin_amdgcn_mov_dpp(v, PAC_DPP_QXOR1, 0xf, 0xf, true));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, PAC_DPP_QXOR2, 0xf, 0xf, true));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, PAC_DPP_HMIRROR, 0xf, 0xf, true));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, PAC_DPP_MIRROR, 0xf, 0xf, true));
+    const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    v = min((int)p[0], (int)p[1]);
+    const auto q = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    v = min((int)q[0], (int)q[1]);
+    return __builtin_amdgcn_readlane(v, 0);
+}
+
 // diagnostic build (-DPAC_ROWPROF): cycle and size counters of the masking rows
 #ifdef PAC_ROWPROF
 __device__ unsigned long long pac_rowprof[1024 * 16];   // spread over 1024 lines: no hot address
@@ -1007,15 +1059,20 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
     RP_T(t1);
     // loud maskers below the line: loud-list ranks [0, Ul)
     const int Ul = L.lpre[U];
-    const int umin = wave_min_i(Ul), umax = wave_max_i(Ul);
+    // U(l) is nondecreasing in l (mask_ku is a two-pointer sweep over the
+    // ascending bark_line; rank and lpre are prefix counts): the row's
+    // extremes are lanes 0 and 63
+    const int umin = __builtin_amdgcn_readlane(Ul, 0), umax = __builtin_amdgcn_readlane(Ul, WAVE - 1);
     double up = 0.0;
     int m0 = umax, ua = umax;
     bool direct = true;
     int D = -1;
     if (umax > 0) {
-        const double lb = wave_ext_f64<false>(((upq + flat) + lower) + tiq);   // I(l) >= lb on every lane
-        // floor(log2 lb) - 64 from the exponent field: a conservative cut
-        const double l2cut = (double)(__builtin_amdgcn_frexp_exp(lb) - 65);
+        // I(l) >= lb = min over the row of ((upq + flat) + lower) + tiq; the cut is
+        // floor(log2 lb) - 64 from the exponent field (conservative).  frexp_exp is
+        // nondecreasing on positive doubles, so the minimum exponent is lb's.
+        const int elb = wave_min0_i(__builtin_amdgcn_frexp_exp(((upq + flat) + lower) + tiq));
+        const double l2cut = (double)(elb - 65);
         for (int base = 0; base < umax; base += WAVE) {   // first loud masker that is not negligible
             const int m = base + lane;
             int keep = 1;
@@ -1043,11 +1100,11 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
         double kmn = INFINITY, kmx = -INFINITY;
         for (int m = m0 + lane; m < ua; m += WAVE) {
             const double k = L.lku[m];
-            kmn = fmin(kmn, k);
-            kmx = fmax(kmx, k);
+            kmn = vmin_f64(kmn, k);
+            kmx = vmax_f64(kmx, k);
         }
-        kmn = wave_ext_f64<false>(kmn);
-        kmx = wave_ext_f64<true>(kmx);
+        kmn = wave_ext0_f64<false>(kmn);
+        kmx = wave_ext0_f64<true>(kmx);
         const double adl = fmax(zm - zr, zt - zm);       // max |z_l - z_mid| over the row
         const double kc = 0.5 * (kmn + kmx);
         const double eps = (0.5 * (kmx - kmn) * adl) * PAC_LN2 * 1.0000001;

@@ -580,6 +580,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "alg_bytes_per_block": ALG_BYTES.get(dom, 4096),
+                     "traffic_unit": "HBM bytes (FETCH_SIZE + WRITE_SIZE) per step, all launches of the kernel; "
+                                     "achieved/alg bytes are per step too",
+                     "traffic_per_block": traffic / blocks if traffic is not None and blocks else None,
                      "traffic_source": prof_note,
                      "note": "%s is FP64-VALU bound (masking sum), not HBM bound: see 'fp64' and "
                              "DESIGN.md section 4" % dom},

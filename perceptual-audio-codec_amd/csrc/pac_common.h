@@ -102,6 +102,32 @@ __device__ __forceinline__ double pac_exp2(double y) {
     p = __builtin_fma(p, f, 1.0);
     return __builtin_ldexp(p, (int)n);
 }
+// The same 2^y (bit-identical: the same fused multiply-adds in the same order)
+// with the Horner steps as VOP3 v_fma_f64 on VGPR coefficients.  Where the
+// coefficients live in VGPRs (SGPR-tight kernels: the masking rows), the
+// compiler otherwise shrinks each step to the two-address v_fmac_f64 and pays
+// a v_mov_b64 copy of the coefficient per step.
+__device__ __forceinline__ double fma_v(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ double pac_exp2_v(double y) {
+    double n = __builtin_rint(y);
+    double f = y - n;
+    double p = 7.072585949269223e-09;
+    p = fma_v(p, f, 1.0208690299958306e-07);
+    p = fma_v(p, f, 1.321544258792169e-06);
+    p = fma_v(p, f, 1.5252657260200837e-05);
+    p = fma_v(p, f, 0.0001540353044173605);
+    p = fma_v(p, f, 0.0013333558230164974);
+    p = fma_v(p, f, 0.009618129107606888);
+    p = fma_v(p, f, 0.05550410866444772);
+    p = fma_v(p, f, 0.24022650695910097);
+    p = fma_v(p, f, 0.69314718055995);
+    p = __builtin_fma(p, f, 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
 
 // log10(x) for positive normal x, ~35 VALU instead of the library's ~100:
 // x = 2^k m, m in [sqrt(1/2), sqrt(2)), ln m = f - (f^2/2 - s (f^2/2 + R(s^2))),

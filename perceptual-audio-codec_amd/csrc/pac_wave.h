@@ -1010,7 +1010,7 @@ __device__ __forceinline__ double mom_group(const MaskerLists& L, const PacTable
         ck[k] = 0.0;
         if (m < ua) {
             const double ku = L.lku[m];
-            pk[k] = pac_exp2(__builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m]));
+            pk[k] = pac_exp2_v(__builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m]));
             ck[k] = ku - kc;
         }
     }
@@ -1124,7 +1124,7 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
                 else if (K == 3) acc += mom_group<3>(L, T, g0, ua, lane, zm, kc, x, D);
                 else acc += mom_group<4>(L, T, g0, ua, lane, zm, kc, x, D);
             }
-            up = acc * pac_exp2(kc * dl);
+            up = acc * pac_exp2_v(kc * dl);
         }
     }
     RP_T(t3);
@@ -1132,13 +1132,13 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
 #pragma unroll 2
         for (int m = m0; m < ua; ++m) {             // m < umin <= Ul on every lane
             const double ku = L.lku[m];
-            up += pac_exp2(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
+            up += pac_exp2_v(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
         }
     }
 #pragma unroll 2
     for (int m = ua; m < umax; ++m) {
         const double ku = L.lku[m];
-        const double t = pac_exp2(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
+        const double t = pac_exp2_v(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
         up += (m < Ul) ? t : 0.0;
     }
     RP_T(t4);

@@ -973,8 +973,11 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
 // codes], LRMS(25) [+ the block-switching bit], MSB-first.  Waves 2c and 2c+1
 // pack channel c, rows 0-7 and 8-15 of its lines; the code-bit prefix crosses
 // the halves through LDS.  A channel-block that would end past cap is
-// skipped; the host reports PAC_E_CAPACITY from the total.
-__global__ __launch_bounds__(256) void k_master_pack(const PacTables* __restrict__ T,
+// skipped; the host reports PAC_E_CAPACITY from the total.  Latency bound
+// (dependent table gathers, barriers): 6 waves per SIMD (<= 80 VGPRs, no
+// spill) instead of the 5 that 96 VGPRs allow, 182 -> 157 ms per 10^7 blocks
+// (7 waves spills; 8 spills more and is slower than 5).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_master_pack(const PacTables* __restrict__ T,
                                                      const PacHuffTables* __restrict__ H, PacMasterFields F,
                                                      int nch, int64_t nblocks, const int64_t* __restrict__ off,
                                                      uint8_t* __restrict__ out, int64_t cap) {

@@ -597,6 +597,27 @@ __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTab
     }
 }
 
+// lane i <- lane i + OFF of its DPP row (row_shl:OFF; bound_ctrl: 0 past the
+// row, never taken: the callers' segments end inside the row)
+template <int OFF>
+__device__ __forceinline__ unsigned long long row_shl_u64(unsigned long long v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)v, 0x100 + OFF, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), 0x100 + OFF, 0xf, 0xf, true);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+template <int OFF>
+__device__ __forceinline__ void seg_max_step(unsigned long long& k0, unsigned long long& k1,
+                                             unsigned long long& k2, unsigned long long& k3, bool take) {
+    const unsigned long long o0 = row_shl_u64<OFF>(k0), o1 = row_shl_u64<OFF>(k1);
+    const unsigned long long o2 = row_shl_u64<OFF>(k2), o3 = row_shl_u64<OFF>(k3);
+    if (take) {
+        k0 = o0 > k0 ? o0 : k0;
+        k1 = o1 > k1 ? o1 : k1;
+        k2 = o2 > k2 ? o2 : k2;
+        k3 = o3 > k3 ? o3 : k3;
+    }
+}
+
 // One 256-thread workgroup per stereo block: MDCT L/R and overall scales, M/S
 // lines, MLD threshold combination, SMR selection and the band maxima (LDS
 // atomic max on order-preserving keys).  Only the thresholds of each band's
@@ -710,27 +731,21 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;
         lines[PAC_HALFN + l] = v1;
-        // band maxima: the wave's 64 consecutive lines hold whole band segments;
-        // a segmented max down to each segment's first lane, then one LDS
-        // atomic per segment (same-address atomics serialise)
+        // band maxima: each DPP row of 16 lines holds whole band pieces; a
+        // segmented max (row_shl DPP, no LDS crossbar) down to each piece's
+        // first lane, then one LDS atomic per piece (same-address atomics
+        // serialise: at most 4 per band and wave)
         const bool in = l < lend;
         const int lane = tid & (WAVE - 1);
-        const int e = in ? min(WAVE - 1, lane + (T->lower[b] + T->nlines[b] - 1 - l)) : lane;
+        const int e = in ? min(lane | 15, lane + (T->lower[b] + T->nlines[b] - 1 - l)) : lane;
         unsigned long long k0 = in ? pac_order_key(d0) : 0ull, k1 = in ? pac_order_key(d1) : 0ull;
         unsigned long long k2 = in ? (unsigned long long)__double_as_longlong(fabs(v0)) : 0ull;
         unsigned long long k3 = in ? (unsigned long long)__double_as_longlong(fabs(v1)) : 0ull;
-#pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-            const unsigned long long o0 = __shfl_down(k0, off, WAVE), o1 = __shfl_down(k1, off, WAVE);
-            const unsigned long long o2 = __shfl_down(k2, off, WAVE), o3 = __shfl_down(k3, off, WAVE);
-            if (lane + off <= e) {
-                k0 = o0 > k0 ? o0 : k0;
-                k1 = o1 > k1 ? o1 : k1;
-                k2 = o2 > k2 ? o2 : k2;
-                k3 = o3 > k3 ? o3 : k3;
-            }
-        }
-        if (in && (lane == 0 || l == T->lower[b])) {
+        seg_max_step<1>(k0, k1, k2, k3, lane + 1 <= e);
+        seg_max_step<2>(k0, k1, k2, k3, lane + 2 <= e);
+        seg_max_step<4>(k0, k1, k2, k3, lane + 4 <= e);
+        seg_max_step<8>(k0, k1, k2, k3, lane + 8 <= e);
+        if (in && ((lane & 15) == 0 || l == T->lower[b])) {
             atomicMax(&key[0][b], k0);
             atomicMax(&key[1][b], k1);
             atomicMax(&key[2][b], k2);

@@ -20,14 +20,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        double w = __shfl_xor(v, o, WAVE);
-        v = w > v ? w : v;
-    }
-    return v;
-}
 
 // Cross-lane moves of a double through DPP (VALU, no LDS round trip).  Lanes
 // outside ROWMASK (or without a source) get `old`.
@@ -931,6 +923,9 @@ __device__ __forceinline__ double wave_ext0_f64(double v) {
     }
     return readlane_f64(v, 0);
 }
+// wave maximum of non-NaN doubles, wave-uniform (DPP + permlane swaps, no
+// ds_bpermute round trips)
+__device__ __forceinline__ double wave_max(double v) { return wave_ext0_f64<true>(v); }
 // integer minimum, the same shape (DPP steps fold into v_min_i32_dpp)
 __device__ __forceinline__ int wave_min0_i(int v) {
     v = min(v, __builtin_amdgcn_mov_dpp(v, PAC_DPP_QXOR1, 0xf, 0xf, true));

@@ -988,11 +988,12 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
 // codes], LRMS(25) [+ the block-switching bit], MSB-first.  Waves 2c and 2c+1
 // pack channel c, rows 0-7 and 8-15 of its lines; the code-bit prefix crosses
 // the halves through LDS.  A channel-block that would end past cap is
-// skipped; the host reports PAC_E_CAPACITY from the total.  Latency bound
-// (dependent table gathers, barriers): 6 waves per SIMD (<= 80 VGPRs, no
-// spill) instead of the 5 that 96 VGPRs allow, 182 -> 157 ms per 10^7 blocks
-// (7 waves spills; 8 spills more and is slower than 5).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_master_pack(const PacTables* __restrict__ T,
+// skipped; the host reports PAC_E_CAPACITY from the total.  Latency bound:
+// a chain of dependent memory round trips, so every load that depends only on
+// the channel-block is issued before the first barrier (182 -> 108 ms per
+// 10^7 blocks with 5 waves per SIMD; 6 waves alone gave 157, 6 with the early
+// loads spills and is no faster).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_master_pack(const PacTables* __restrict__ T,
                                                      const PacHuffTables* __restrict__ H, PacMasterFields F,
                                                      int nch, int64_t nblocks, const int64_t* __restrict__ off,
                                                      uint8_t* __restrict__ out, int64_t cap) {
@@ -1006,6 +1007,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const int c = w >> 1, h = w & 1;
     const int64_t gb = xcd_item(blockIdx.x, nblocks);
     const int fl = F.bsf ? F.bsf[gb] : 0;
+    const bool act = c < nch;                  // mono: waves 2, 3 only zero the words and meet the barriers
+    const int64_t g = gb * nch + (act ? c : 0);
+    // every load that depends on nothing but g first (the kernel is a chain of
+    // dependent memory round trips): table id, this wave's codes and band
+    // indices, the byte count and offset of the store at the end
+    const int tb = F.tid[g] - 1;
+    const int nb = F.nbytes[g];
+    const int64_t og = off[g];
+    const uint16_t* cm = F.codes + g * PAC_HALFN;
+    uint32_t mc[8];
+    int bl[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int l = (8 * h + q) * WAVE + lane;
+        bl[q] = T->band_of_line[l];
+        mc[q] = cm[l];                         // 0 where ba == 0 (k_master_tail)
+    }
     if (tid < PAC_NB) lr[tid] = F.lrms[gb * PAC_NB + tid];
     if (tid < nch * PAC_NB) {
         const int cc = tid / PAC_NB, b = tid % PAC_NB;
@@ -1017,22 +1035,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         words[1][i] = 0u;
     }
     __syncthreads();
-    const bool act = c < nch;                  // mono: waves 2, 3 only zero the words and meet the barriers
-    const int64_t g = gb * nch + (act ? c : 0);
-    const int tb = F.tid[g] - 1;
-    const uint16_t* cm = F.codes + g * PAC_HALFN;
     // this wave's 8 rows: sign + code of length clen per line (0 for ba == 0 bands)
     uint32_t code[8], sgn[8];
     int clen[8], esc[8], pre[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int l = (8 * h + q) * WAVE + lane;
-        const int b = T->band_of_line[l];
+        const int b = bl[q];
         const int ba = bas[c][b];
         clen[q] = 0; esc[q] = 0; code[q] = 0; sgn[q] = 0;
         uint32_t m = 0;
         if (ba && act) {
-            m = cm[l];
+            m = mc[q];
             const uint32_t sym = m & ((1u << (ba - 1)) - 1u);
             sgn[q] = (m >> (ba - 1)) & 1u;
             const int L = H->len[tb][sym];
@@ -1072,7 +1086,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int l = (8 * h + q) * WAVE + lane;
-        const int b = T->band_of_line[l];
+        const int b = bl[q];
         if (act && l == T->lower[b] && T->nlines[b]) pal[c][b] = pre[q];
     }
     __syncthreads();
@@ -1104,7 +1118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int l = (8 * h + q) * WAVE + lane;
-        const int b = T->band_of_line[l];
+        const int b = bl[q];
         const int ba = act ? bas[c][b] : 0;
         if (!ba) continue;
         const int p0 = bstart[c][b] + pal[c][b] + 8;
@@ -1119,9 +1133,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
     }
     __syncthreads();
-    const int nb = F.nbytes[g];
-    if (!act || off[g] + nb > cap) return;
-    uint8_t* o = out + off[g];
+    if (!act || og + nb > cap) return;
+    uint8_t* o = out + og;
     if (h == 0 && lane < 4) o[lane] = (uint8_t)((uint32_t)(nb - 4) >> (8 * lane));   // '<L' nBytes
     for (int i = h * WAVE + lane; i < nb - 4; i += 2 * WAVE) o[4 + i] = be_byte(wd, i);
 }

@@ -475,6 +475,16 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
     const int tid = threadIdx.x;
     const int64_t g = xcd_item(blockIdx.x, G);
     const BlockRef r = locate(src, g / src.n_ch, (int)(g % src.n_ch));
+    // loads that depend only on g, issued before the MDCT (latency-bound chain)
+    const int overall = W.overall[g];
+    const int nbytes = W.nbytes[g] - 4;
+    const int64_t og = off[g];
+    int bl[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        bl[j] = T->band_of_line[j * FRONT_NT + tid];
+        lo[j] = T->lower[bl[j]];
+    }
     for (int i = tid; i < PACK_WORDS; i += FRONT_NT) words[i] = 0;
     if (tid < PAC_NB) {
         bas[tid] = W.ba[g * PAC_NB + tid];
@@ -488,7 +498,6 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
         for (int b = 0; b < PAC_NB; ++b) { start[b] = p; p += 8 + bas[b] * T->nlines[b]; }
     }
     __syncthreads();
-    const int overall = W.overall[g];
     const double gain = (double)(1 << overall);
     if (tid == 0) put_bits(words, 0, (uint32_t)overall, 4);
     if (tid < PAC_NB) {
@@ -499,17 +508,16 @@ __global__ __launch_bounds__(FRONT_NT) void k_origin_pack(PacSource src, const P
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         int l = j * FRONT_NT + tid;
-        int b = T->band_of_line[l];
+        int b = bl[j];
         int ba = bas[b];
         if (ba) {
             uint32_t m = pac_mantissa(X[l] * gain, sfs[b], ba);
-            put_bits(words, start[b] + 8 + (l - T->lower[b]) * ba, m, ba);
+            put_bits(words, start[b] + 8 + (l - lo[j]) * ba, m, ba);
         }
     }
     __syncthreads();
-    const int nbytes = W.nbytes[g] - 4;
-    if (off[g] + 4 + nbytes > cap) return;     // host reports PAC_E_CAPACITY from the total
-    uint8_t* o = out + off[g];
+    if (og + 4 + nbytes > cap) return;     // host reports PAC_E_CAPACITY from the total
+    uint8_t* o = out + og;
     if (tid < 4) o[tid] = (uint8_t)((uint32_t)nbytes >> (8 * tid));   // '<L' nBytes
     for (int i = tid; i < nbytes; i += FRONT_NT) o[4 + i] = be_byte(words, i);
 }

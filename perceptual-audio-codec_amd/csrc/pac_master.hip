@@ -458,6 +458,22 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     const int64_t gb = cp.gb;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
+    // the leaf and band tables, loaded before the FFTs (their round trips
+    // overlap the transform instead of following it)
+    const int lf = tid >> 2, sub = tid & 3;
+    const bool has = lf < T->lr_nleaf;
+    int e0 = 0, n = 0, lo = 0;
+    if (has) {
+        e0 = T->lr_leaf_e0[lf];
+        n = T->lr_leaf_n[lf];
+        lo = T->lower[T->lr_leaf_band[lf]];
+    }
+    int fl0 = 0, nlb = 0, lob = 0;
+    if (tid < PAC_NB) {
+        fl0 = T->lr_first_leaf[tid];
+        nlb = T->nlines[tid];
+        lob = T->lower[tid];
+    }
     if (!rL.f) {
         grp_spectrum_cplx2p<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
             const double2 f0 = stereo_frame(rL, 2 * n), f1 = stereo_frame(rL, 2 * n + 1);
@@ -477,14 +493,6 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     // r[2 sub], r[2 sub + 1] (complex elements e0 + 4 k + sub) in order, the
     // quad then combines ((r0 + r2) + (r4 + r6)) by DPP, lane 0 adds the tail
     // elements: numpy's exact operation order
-    const int lf = tid >> 2, sub = tid & 3;
-    const bool has = lf < T->lr_nleaf;
-    int e0 = 0, n = 0, lo = 0;
-    if (has) {
-        e0 = T->lr_leaf_e0[lf];
-        n = T->lr_leaf_n[lf];
-        lo = T->lower[T->lr_leaf_band[lf]];
-    }
     auto zz = [&](int e, double2& d, double2& sm) {
         const double2 a = sq(bufA[lo + e]), c = sq(bufB[lo + e]);
         d = make_double2(__dsub_rn(a.x, c.x), __dsub_rn(a.y, c.y));
@@ -525,14 +533,14 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     if (tid < WAVE) {                              // wave 0: the decisions and the rows they select
         int rows = 0;
         if (tid < PAC_NB) {
-            int i0 = T->lr_first_leaf[tid], i1 = i0;
-            const int nl = T->nlines[tid];
+            int i0 = fl0, i1 = i0;
+            const int nl = nlb;
             const double2 sd = np_csum_combine<5>(leafv0, i0, 2 * nl);
             const double2 ss = np_csum_combine<5>(leafv1, i1, 2 * nl);
             const int ms = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
             F.lrms[gb * PAC_NB + tid] = (uint8_t)ms;
             if (nl) {                              // the 64-line rows of the band's lines
-                const int r0 = T->lower[tid] / WAVE, r1 = (T->lower[tid] + nl - 1) / WAVE;
+                const int r0 = lob / WAVE, r1 = (lob + nl - 1) / WAVE;
                 rows = ((2 << r1) - (1 << r0)) << (ms ? 16 : 0);
             }
         }

@@ -56,6 +56,25 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
 INPUTS = os.path.join(ROOT, "tests", "fixtures", "inputs")
 
 
+def host_cores():
+    """CPUs this process may use: the affinity set, capped by the host's
+    OMP_NUM_THREADS share when set (the GPU box exports 16 and shows the whole
+    machine's CPUs in the affinity set)"""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+# the reference Python itself, timed in the survey container (BASELINE.md):
+# it cannot run on the GPU box (Python 2 source, /root/reference absent there)
+REF_PYTHON = {"master": {"value": 11.0, "unit": "blocks/s", "cores": 1,
+                         "sample": "BASELINE.md: reference codec/ (Py3 semantics shim) on inputs/harpsichord.wav, "
+                                   "387 blocks, 1 core of the survey container's Xeon"},
+              "origin": {"value": 18.1, "unit": "blocks/s", "cores": 1,
+                         "sample": "BASELINE.md: reference PerceptualAudioCodec_Origin/codec/ on "
+                                   "inputs/harpsichord.wav, 387 blocks, 1 core of the survey container's Xeon"}}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,12 +95,16 @@ def parse():
     ap.add_argument("--sample-rate", type=int, default=48000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (oracle on host cores)")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="host threads of the CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="host threads of the CPU baseline (default: the CPUs this process may run on, "
+                         "os.sched_getaffinity, capped by OMP_NUM_THREADS when the host sets it -- the "
+                         "GPU box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     if a.profile is not None:
         a.config = 1 if a.profile == "origin" else 2
+    if a.cpu_threads is None:
+        a.cpu_threads = host_cores()
     a.master = a.config != 1
     a.bs = a.config == 4
     a.profile = "master" if a.master else "origin"
@@ -142,9 +165,17 @@ class Dist:
 # rate at the reference algorithm's flop count.
 REF_ALG_FLOP_PER_BLOCK = {"origin": 18.0e6, "master": 48.0e6}
 
-# Algorithmic HBM bytes per stereo block of each kernel:
-# what the kernel must read and write, not what it happens to move.
-ALG_BYTES = {
+# Algorithmic HBM bytes per stereo block: the
+# 4096 B of int16 PCM read + the packed bitstream written (the measured
+# out_bytes / blocks, ~592 B for configs[2]) -- the whole path's bytes, and
+# the numerator of roofline.achieved for the dominant kernel too.
+PCM_BYTES_PER_BLOCK = 2 * 1024 * 2
+
+# What each kernel of OUR kernel split reads and writes per stereo block
+# (inputs + outputs, incl. the intermediates another kernel produced or
+# consumes: spectra, threshold rows, MDCT lines).  Not algorithmic bytes --
+# reported as roofline.kernel_io_bytes_per_block beside them.
+KERNEL_IO_BYTES = {
     "k_origin_front": 4096 + 2 * (25 * 8 * 2 + 1),   # int16 PCM in; SMR + band peaks + overall out
     "k_master_spec": 4096 + 2 * 1025 * 16,           # int16 PCM in; FFT bins 0..1024 of a and b out
     "k_master_thr": 2 * 1025 * 16 + 6 * 1024 * 8,    # the spectra in; 6 threshold rows out (calcBTHR x 6)
@@ -152,6 +183,20 @@ ALG_BYTES = {
     "k_master_tail": 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2 * (25 * 2 + 1 + 4 + 8),
     "k_master_pack": 2 * 1024 * 8 + 2 * 25 * 2 + 25 + 2 + 2 * 300,
 }
+
+
+def master_launches(nb, chunk_blocks=65536):
+    """launches of each pass-1 master kernel per pac_encode_streams call of
+    streams with nb[i] blocks: one per chunk (run_master in pac_abi.hip:
+    groups of <= chunk_blocks streams, S = min(chunk_blocks / n_s, longest
+    stream) blocks per stream per chunk)"""
+    n = 0
+    for g0 in range(0, len(nb), chunk_blocks):
+        grp = nb[g0:g0 + chunk_blocks]
+        gmax = max(1, max(grp))
+        S = max(1, min(chunk_blocks // len(grp), gmax))
+        n += (gmax + S - 1) // S
+    return n
 
 
 def measured_profile(kind, kernel):
@@ -209,6 +254,8 @@ def cpu_baseline(ctx, samples, fs, seconds, profile, threads, bs=False):
     el = time.perf_counter() - t0
     done = sum(r[0] for r in res)
     base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": len(os.sched_getaffinity(0)),
+            "reference_python": REF_PYTHON[profile],
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
                       "fixtures), %s profile%s, %d host threads (one stream each, growing prefixes), "
                       "%d stereo blocks of the same streams in %.1f s"
@@ -250,7 +297,8 @@ class Job:
     def __init__(self, ctx, p, fo, pcm_dev):
         self.ctx, self.p, self.fo, self.pcm_dev = ctx, p, fo, pcm_dev
         self.ns = len(fo) - 1
-        self.blocks = int(sum(shard.blocks_of(fo[i + 1] - fo[i]) for i in range(self.ns)))
+        self.bcounts = [shard.blocks_of(int(fo[i + 1] - fo[i])) for i in range(self.ns)]
+        self.blocks = int(sum(self.bcounts))
         # the worst case (pac_encode_bound: 6 KB per master channel-block) would
         # be 120 GB at 10^7 blocks; 1 KB per channel-block is > 3x the real
         # average, and the library refuses (PAC_E_CAPACITY), never overflows
@@ -293,7 +341,8 @@ class WavJob(Job):
         for j, b in enumerate(blobs):        # upload file by file (no host copy of the whole batch)
             ctx.to_device(self.blob_dev + int(self.foff[j]), np.frombuffer(b, dtype=np.uint8))
         info = ctx.wav_scan(self.blob_dev, self.foff, blob_is_device=True)
-        self.blocks = int(sum(shard.blocks_of(w.frames) for w in info))
+        self.bcounts = [shard.blocks_of(w.frames) for w in info]
+        self.blocks = int(sum(self.bcounts))
         self.frames_host = frames_host
         self.cap = self.blocks * p.n_channels * 1024
         self.out_dev = ctx.alloc(self.cap)
@@ -520,18 +569,20 @@ def main():
     # a second stream, overlapped with the next chunk's thresholds)
     dom = max((k for k in kern_ms if k != "k_master_tail"), key=kern_ms.get)
     dom_s = kern_ms[dom] / 1e3
-    alg_bytes = blocks * ALG_BYTES.get(dom, 4096)
-    achieved = alg_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
-    prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
-    traffic = None
-    ref_flop = REF_ALG_FLOP_PER_BLOCK[a.profile]
     step_s = el_max / a.steps
+    # algorithmic bytes = PCM read + bitstream written, per block
+    alg_per_block = PCM_BYTES_PER_BLOCK + out_bytes / blocks
+    launches = sum(master_launches(j.bcounts) for j in jobs) if a.master and dom != "k_master_pack" else len(jobs)
+    achieved = alg_per_block * blocks / dom_s / 1e9 if dom_s > 0 else 0.0
+    prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
+    traffic_pb = None
+    ref_flop = REF_ALG_FLOP_PER_BLOCK[a.profile]
     fp64 = {"ref_alg_flop_per_block": ref_flop,
             "ref_alg_equiv_tflops": ref_flop * blocks / step_s / 1e12 if step_s else None,
             "peak_tflops": FP64_PEAK_TFLOPS, "profile": prof_note}
     if prof:
         if "hbm_read_bytes_per_block" in prof:
-            traffic = (prof["hbm_read_bytes_per_block"] + prof["hbm_write_bytes_per_block"]) * blocks
+            traffic_pb = prof["hbm_read_bytes_per_block"] + prof["hbm_write_bytes_per_block"]
         if "fp64_flop_per_block" in prof:
             tf = prof["fp64_flop_per_block"] * blocks / dom_s / 1e12
             fp64.update({"kernel": dom, "executed_flop_per_block": prof["fp64_flop_per_block"],
@@ -539,6 +590,30 @@ def main():
         for k in ("valu_issue_util", "fp64_share_of_valu", "lds_bank_conflict_frac"):
             if k in prof:
                 fp64[k] = prof[k]
+    roofline = {
+        "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic_pb * blocks / launches if traffic_pb is not None else None,
+        "alg_bytes_per_block": alg_per_block,
+        "alg_bytes_def": "SURVEY.md 8(d): 4096 B int16 PCM read + the measured bitstream bytes written "
+                         "(out_bytes_per_gpu / blocks_per_gpu)",
+        "launches_per_step": launches, "blocks_per_launch": blocks / launches,
+        "alg_bytes_per_launch": alg_per_block * blocks / launches,
+        "avg_launch_ms": kern_ms[dom] / launches,
+        "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/summarize_pmc.py), "
+                        "same source hash only",
+        "traffic_per_block": traffic_pb,
+        "traffic_over_alg": traffic_pb / alg_per_block if traffic_pb is not None else None,
+        "traffic_source": prof_note,
+        "kernel_io_bytes_per_block": KERNEL_IO_BYTES.get(dom),
+        "kernel_io_def": "what this kernel of our split reads + writes per block, intermediates included "
+                         "(not algorithmic)",
+        "step": {"achieved": alg_per_block * blocks / step_s / 1e9,
+                 "frac": alg_per_block * blocks / step_s / 1e9 / HBM_PEAK_GBS},
+        "binding": {"resource": "fp64-valu", "executed_frac": fp64.get("executed_frac"),
+                    "note": "%s is bound by FP64 VALU issue (the masking sums), not by HBM: the HBM "
+                            "fraction is small by construction (SURVEY.md 8(d), DESIGN.md section 4)" % dom},
+    }
     if a.config == 2:
         data = "synthetic (device-generated pink noise (Voss, counter hash) + 440/1250/5300 Hz tones)"
         workload = ("BASELINE configs[2]: synthetic 48 kHz stereo pink noise + tones, %d stereo blocks per GPU "
@@ -576,16 +651,8 @@ def main():
         "data": data,
         "config": {"workload": workload, "profile": a.profile, "global_blocks": int(total_blocks),
                    "blocks_per_gpu": blocks, "parallelism": "streams sharded, %d rank(s), no collective"
-                   % dist.world},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "alg_bytes_per_block": ALG_BYTES.get(dom, 4096),
-                     "traffic_unit": "HBM bytes (FETCH_SIZE + WRITE_SIZE) per step, all launches of the kernel; "
-                                     "achieved/alg bytes are per step too",
-                     "traffic_per_block": traffic / blocks if traffic is not None and blocks else None,
-                     "traffic_source": prof_note,
-                     "note": "%s is FP64-VALU bound (masking sum), not HBM bound: see 'fp64' and "
-                             "DESIGN.md section 4" % dom},
+                   % dist.world, "tail_mode": os.environ.get("PAC_TAIL_MODE", "overlap")},
+        "roofline": roofline,
         "fp64": fp64,
         "kernels_ms": kern_ms,
         "out_bytes_per_gpu": out_bytes,

@@ -17,6 +17,20 @@ ERRORS = {-1: "PAC_E_ARG", -2: "PAC_E_HIP", -3: "PAC_E_NOMEM", -4: "PAC_E_UNSUPP
           -5: "PAC_E_TABLES", -6: "PAC_E_CAPACITY"}
 
 
+PAC_E_ARG = -1
+# pac_wav_info.status -> the reference's PCMFile raise (pcmfile.py:36-51), as
+# wav_status_msg in csrc/pac_abi.hip
+WAV_STATUS = {-1: "File opened for PCMFile is not a RIFF file!",
+              -2: "Didn't find WAV file 'fmt ' chunk following RIFF file header",
+              -3: "Opened a non-PCM WAV file as a PCMFile",
+              -4: "PCMFile was not 16-bits per sample",
+              -5: "Didn't find WAV file 'data' chunk following 'fmt ' chunk"}
+
+
+def wav_status_message(status):
+    return WAV_STATUS.get(status, "malformed WAV file")
+
+
 class PacError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("%s: %s" % (ERRORS.get(code, code), msg))
@@ -269,10 +283,13 @@ class Context:
             arr = np.frombuffer(blob, dtype=np.uint8)
             ptr = arr.ctypes.data
         if out is None:
-            # >= pac_encode_bound of any 16-bit file: per 2048 bytes at most one
-            # mono block (or half a stereo one) of <= 6054 bytes, + flush/quirk hops
-            cap = sum((int(fo[i + 1] - fo[i]) // 2048 + 3) * 6100 for i in range(n))
-            out = np.empty(cap, dtype=np.uint8)
+            # pac_encode_bound over the frames the device scan finds (a bad file
+            # counts 0: the encode call reports it)
+            scan = self.wav_scan(blob, fo, blob_is_device=blob_is_device)
+            ffo = np.zeros(n + 1, dtype=np.int64)
+            ffo[1:] = np.cumsum([w.frames if w.status == 0 else 0 for w in scan])
+            cap = int(self.L.pac_encode_bound(C.byref(params), n, ffo.ctypes.data_as(C.POINTER(C.c_int64))))
+            out = np.empty(max(cap, 1), dtype=np.uint8)
         if isinstance(out, np.ndarray):
             out_ptr, cap = out.ctypes.data, (out.nbytes if out_capacity is None else out_capacity)
         else:

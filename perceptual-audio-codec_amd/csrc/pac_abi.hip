@@ -306,6 +306,7 @@ struct pac_ctx {
     hipStream_t stream = nullptr;
     std::map<int, PacTables*> tables;  // device tables per sample rate
     PacHuffTables* huff = nullptr;     // device
+    DevBuf<uint32_t> hscore;           // [PAC_HSC_N][PAC_HSC_W] per-(ba, symbol) costs of the ten tables (k_master_tail)
     bool have_huff = false;
     // work
     DevBuf<double> smr, bandpeak;
@@ -336,6 +337,10 @@ struct pac_ctx {
     // no longer gains (3.71 vs 3.72 M blocks/s) and in line every kernel's
     // event time is its own (clean per-kernel rooflines)
     bool lrms_async = false;
+    // PAC_TAIL_MODE=serial: the reservoir tail of each chunk on `stream`
+    // right after the chunk's front kernels (nothing co-runs) -- the
+    // measurement baseline of the default placement (run_master)
+    bool tail_serial = false;
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
     DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)
@@ -375,9 +380,11 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     HIPCHK(hipSetDevice(device));
     pac_ctx* c = new pac_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+    if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
+    const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+                    hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
+                    hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
     }
@@ -396,6 +403,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamSynchronize(c->stream2);
     hipStreamSynchronize(c->stream3);
     for (auto& kv : c->tables) hipFree(kv.second);
+    c->hscore.release();
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
@@ -485,18 +493,30 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
             h->bits[tid - 1][sym] = b;
         }
     }
-    for (int sym = 0; sym < PAC_NSYM; sym++) {
-        uint64_t v = 0;
-        for (int t = 0; t < PAC_NTAB; t++) {
-            if (h->len[t][sym] > 30) {
+    for (int sym = 0; sym < PAC_NSYM; sym++)
+        for (int t = 0; t < PAC_NTAB; t++)
+            if (h->len[t][sym] > 30) {     // the pack's 64-bit bit windows and the 16-bit scoring sums assume it
                 free(h);
                 return set_err(PAC_E_TABLES, "code longer than 30 bits");
             }
-            v |= (uint64_t)h->len[t][sym] << (5 * t);
+    // the tail's scoring table: for each ba = 2..16 and symbol < 2^(ba-1), the
+    // ten tables' code lengths, or escape length + ba (Huffman.py:284-300)
+    std::vector<uint32_t> hs((size_t)PAC_HSC_N * PAC_HSC_W, 0u);
+    for (int ba = 2; ba <= 16; ba++)
+        for (int sym = 0; sym < (1 << (ba - 1)); sym++) {
+            uint32_t* ent = hs.data() + (size_t)(((1 << (ba - 1)) - 2) + sym) * PAC_HSC_W;
+            for (int t = 0; t < PAC_NTAB; t++) {
+                const uint32_t cost = h->len[t][sym] ? h->len[t][sym] : (uint32_t)(h->esc_len[t] + ba);
+                ent[t >> 1] |= cost << (16 * (t & 1));
+            }
         }
-        h->lens10[sym] = v;
-    }
     HIPCHK(hipSetDevice(c->device));
+    int rc3;
+    if ((rc3 = c->hscore.ensure(hs.size()))) { free(h); return rc3; }
+    if (hipMemcpy(c->hscore.p, hs.data(), hs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        free(h);
+        return set_err(PAC_E_HIP, "huffman scoring table upload");
+    }
     if (!c->huff && hipMalloc((void**)&c->huff, sizeof(PacHuffTables)) != hipSuccess) {
         free(h);
         return set_err(PAC_E_NOMEM, "device huffman tables");
@@ -801,7 +821,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         F.dbg_code = c->dbg_code.p;
         F.dbg_len = c->dbg_len.p;
     }
-    hipStream_t s0 = c->stream, s1 = c->stream2, s2 = c->stream3;
+    hipStream_t s0 = c->stream, s1 = c->tail_serial ? c->stream : c->stream2, s2 = c->stream3;
     const bool lrms_async = c->lrms_async && nch == 2;
     const double budget = bit_budget(p);
     // timing: events recorded around every launch on its own stream, read
@@ -821,6 +841,28 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     HIPCHK(hipEventRecord(c->evs[4], s0));            // states and tables are on s0
     HIPCHK(hipStreamWaitEvent(s1, c->evs[4], 0));
     if (lrms_async) HIPCHK(hipStreamWaitEvent(s2, c->evs[4], 0));
+    // The tail of chunk i runs on s1 once chunk i+1's spectra are done, i.e.
+    // next to chunk i+1's threshold kernel: k_master_thr holds 4 waves per
+    // SIMD (104 of 512 VGPRs each) and the tail (<= 96 VGPRs, one wave per
+    // workgroup, 256 B of LDS) fills the fifth slot without displacing a
+    // threshold workgroup.  Launched right after chunk i's front instead, it
+    // shares the CUs with chunk i+1's LRMS kernel (5 workgroups per CU), which
+    // then runs at half speed.
+    struct Pend { PacMasterChunk ck; PacMasterChunkBuf K; int k, n_s; };
+    std::vector<Pend> pend;
+    auto launch_tail = [&](const Pend& t) -> int {
+        int rc2;
+        HIPCHK(hipEventRecord(c->evs[t.k], s0));
+        HIPCHK(hipStreamWaitEvent(s1, c->evs[t.k], 0));
+        if ((rc2 = mark(1, -1))) return rc2;
+        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((t.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS, s1, T,
+                           c->hscore.p, t.K, F,
+                           c->blk_off.p, t.ck, c->st_extra.p, c->st_deposit.p, budget);
+        HIPCHK(hipGetLastError());
+        if ((rc2 = mark(1, 2))) return rc2;
+        HIPCHK(hipEventRecord(c->evs[2 + t.k], s1));
+        return PAC_OK;
+    };
     int64_t i = 0;
     for (const Grp& gr : groups) {
         for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S, ++i) {
@@ -849,6 +891,10 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             }
             hipLaunchKernelGGL(k_master_spec, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             if ((rc = mark(0, 7))) return rc;
+            if (!pend.empty()) {                  // the previous chunk's tail, next to this chunk's thresholds
+                if ((rc = launch_tail(pend.back()))) return rc;
+                pend.clear();
+            }
             hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
                                T, K, F, ck);
             if ((rc = mark(0, 0))) return rc;
@@ -860,17 +906,14 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
             HIPCHK(hipGetLastError());
             if ((rc = mark(0, 1))) return rc;
-            HIPCHK(hipEventRecord(c->evs[k], s0));
-            HIPCHK(hipStreamWaitEvent(s1, c->evs[k], 0));
-            if ((rc = mark(1, -1))) return rc;
-            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((gr.n_s + 3) / 4)), dim3(WAVE), 0, s1, T,
-                               c->huff, K, F,
-                               c->blk_off.p, ck, c->st_extra.p, c->st_deposit.p, budget);
-            HIPCHK(hipGetLastError());
-            if ((rc = mark(1, 2))) return rc;
-            HIPCHK(hipEventRecord(c->evs[2 + k], s1));
+            pend.push_back({ck, K, k, gr.n_s});
+            if (c->tail_serial) {
+                if ((rc = launch_tail(pend.back()))) return rc;
+                pend.clear();
+            }
         }
     }
+    if (!pend.empty() && (rc = launch_tail(pend.back()))) return rc;
     HIPCHK(hipEventRecord(c->evs[4], s1));
     HIPCHK(hipStreamWaitEvent(s0, c->evs[4], 0));
     // pass 2: byte offsets in file order, then the packing

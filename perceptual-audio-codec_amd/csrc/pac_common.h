@@ -75,9 +75,6 @@ struct PacHuffTables {
     uint32_t bits[PAC_NTAB][PAC_NSYM];
     int32_t esc_len[PAC_NTAB];
     uint32_t esc_bits[PAC_NTAB];
-    // the 10 tables' code lengths of each symbol, 5 bits each (table t at bit
-    // 5 t; lengths <= 30): one gather per line for the table scoring
-    uint64_t lens10[PAC_NSYM];
 };
 
 // ---------------------------------------------------------------------------

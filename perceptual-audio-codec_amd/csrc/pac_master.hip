@@ -17,7 +17,7 @@
 //   k_master_front  one workgroup per block: MDCT L/R + overall scale
 //                   (codec.py:237-246), M/S lines, MLD combination and per-band
 //                   SMR selection (psychoac.py:533-682)
-//   k_master_tail   16 lanes per STREAM of the chunk, its blocks in order:
+//   k_master_tail   one lane per STREAM of the chunk, its blocks in order:
 //                   withdrawBits, the two BitAlloc calls with the extraBits carry
 //                   (codec.py:222-260, bitalloc.py:129-184), scale factors,
 //                   mantissas, 10-table Huffman length scoring, depositBits
@@ -770,122 +770,128 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     }
 }
 
-// --- the reservoir tail: 16 lanes (one DPP row) per stream -----------------
-// Reductions inside a row of 16 lanes: every lane of the row gets the result.
-template <int CTRL>
-__device__ __forceinline__ int dpp_row_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true); }
-__device__ __forceinline__ int row_sum_i(int v) {
-    v += dpp_row_i<PAC_DPP_QXOR1>(v);
-    v += dpp_row_i<PAC_DPP_QXOR2>(v);
-    v += dpp_row_i<PAC_DPP_HMIRROR>(v);
-    v += dpp_row_i<PAC_DPP_MIRROR>(v);
-    return v;
-}
-// (value, band, bits) with the larger value winning, the lower band on a tie
-// (np.argmax's first index over ascending bands)
-template <int CTRL>
-__device__ __forceinline__ void argmax_step(double& v, int& b, int& n) {
-    const double ov = dpp_full_f64<CTRL>(v);
-    const int ob = dpp_row_i<CTRL>(b), on = dpp_row_i<CTRL>(n);
-    const bool take = ov > v || (ov == v && ob < b);
-    v = take ? ov : v;
-    b = take ? ob : b;
-    n = take ? on : n;
-}
-__device__ __forceinline__ void row_argmax(double& v, int& b, int& n) {
-    argmax_step<PAC_DPP_QXOR1>(v, b, n);
-    argmax_step<PAC_DPP_QXOR2>(v, b, n);
-    argmax_step<PAC_DPP_HMIRROR>(v, b, n);
-    argmax_step<PAC_DPP_MIRROR>(v, b, n);
-}
+// --- the reservoir tail: one lane per stream ------------------------------
+// The tail's work is a serial chain per stream (withdrawBits -> BitAlloc ->
+// quantizer -> Huffman length scoring -> depositBits -> the next block), and
+// it runs beside the next chunk's threshold kernel, whose VALU issue it
+// shares: what it costs the pipeline is its VALU instruction count, not its
+// latency.  So every lane runs one stream's chain in program order, as the
+// reference's per-block calls do (no cross-lane reductions: 64 streams per
+// wave instruction), with the per-band state in LDS columns (band-major,
+// lane-minor: every lane's dynamically indexed access is conflict-free).
 
-// master BitAlloc (bitalloc.py:129-184) by the 16 lanes of a row: lane q owns
-// bands q and q + 16.  Each round gives one bit to the first band with the
-// largest smr - 6 bits among the still-valid bands; the stop test uses the
-// max of smr - 6 (bits - 1) over ALL bands as the reference does -- that is
-// max(best valid, best frozen) + 6, the frozen (invalidated) bands' values no
-// longer changing.  The winner's bits, LRMS flag and line count travel with
-// the reduction (no memory access inside the loop).  *ba0 / *ba1 = the lane's
-// bands' allocation; returns the bits left minus extra (same in every lane of
-// the row).
-__device__ __forceinline__ long bitalloc_master_row(const double* __restrict__ smr_g,
-                                                    const uint8_t* __restrict__ lrms,
-                                                    const PacTables* __restrict__ T, double bitBudget, long extra,
-                                                    int maxMantBits, int q, int* ba0, int* ba1) {
-    const int b0 = q, b1 = q + 16;
-    const bool has1 = b1 < PAC_NB;
-    const double s0 = smr_g[b0], s1 = has1 ? smr_g[b1] : 0.0;
-    const int nl0 = T->nlines[b0], nl1 = has1 ? T->nlines[b1] : 0;
-    const int info0 = (lrms[b0] << 5) | (nl0 << 6), info1 = has1 ? ((lrms[b1] << 5) | (nl1 << 6)) : 0;
-    int n0 = 0, n1 = 0;
-    bool v0 = true, v1 = has1;
+// Huffman length scoring table (built by pac_huffman_load): for a band of ba
+// bits, symbol sym < 2^(ba-1), entry ((1 << (ba - 1)) - 2) + sym holds the
+// ten tables' costs of coding it -- the code length, or the escape code's
+// length + ba when the table lacks the symbol (Huffman.py:284-300) -- as
+// 16-bit fields, table t at bits 16 (t & 1) of dword t / 2 (dword 5 unused).
+// A channel-block's sums stay below 1024 * 46 < 2^16, so five 32-bit adds
+// per line score all ten tables.
+#define PAC_HSC_W 6
+#define PAC_HSC_N 65534     // sum over ba = 2..16 of 2^(ba-1)
+
+// BitAlloc (bitalloc.py:129-184) of one channel-block in one lane: each round
+// gives one bit to the first band with the largest SMR - 6 bits among the
+// valid ones (np.argmax); the stop test takes max(SMR - (bits - 1) 6) over ALL
+// bands -- the valid ones' maximum is the chosen band's (the map is monotone),
+// the invalid ones' is the running max of their frozen values.  cur[b][lane]
+// = SMR - 6 bits (one rounding, as the reference's expression), -inf once the
+// band is invalid.  Returns the bits left minus extra; bits[b][lane] = the
+// allocation.
+__device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)[WAVE], uint8_t (*bits)[WAVE],
+                                              const int* __restrict__ nl_s, const double* __restrict__ smr_g,
+                                              uint32_t lrms_bits, double bitBudget, long extra, int maxMantBits,
+                                              int lane) {
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        const double v = smr_g[b];
+        smr[b][lane] = v;
+        cur[b][lane] = v;
+        bits[b][lane] = 0;
+    }
     long total = (long)(bitBudget + (double)extra);
     double frozen = -INFINITY;
     while (true) {
-        double v = v0 ? s0 - n0 * 6. : -INFINITY;
-        int b = v0 ? b0 : 64, p = info0 | n0;
-        if (v1 && s1 - n1 * 6. > v) { v = s1 - n1 * 6.; b = b1; p = info1 | n1; }
-        row_argmax(v, b, p);
-        if (b >= PAC_NB) break;                       // no valid band left (uniform in the row)
-        const int n = p & 31, lri = (p >> 5) & 1, nli = p >> 6;
-        const double gall = fmax(v, frozen) + 6.0;
-        bool drop = gall < (lri ? -5.0 : -15.0);
-        double after = v;
-        if (total - nli >= 0) {
-            if (b == b0) n0 += 1;
-            if (b == b1) n1 += 1;
-            total -= nli;
-            drop |= n + 1 >= maxMantBits;
-            after = v - 6.0;
+        // the maximum, then its first band (the values read twice from LDS:
+        // VALU is what the tail shares with the threshold kernel, and 25 live
+        // doubles would push it past the 96 VGPRs it may use beside it)
+        double best = -INFINITY;
+#pragma unroll
+        for (int b = 0; b < PAC_NB; ++b) best = vmax_f64(best, cur[b][lane]);
+        if (best == -INFINITY) break;                  // no valid band left
+        int ib = 0;
+#pragma unroll
+        for (int b = PAC_NB - 1; b >= 0; --b) ib = cur[b][lane] == best ? b : ib;   // the first maximum
+        const int n = bits[ib][lane], nl = nl_s[ib];
+        const double sv = smr[ib][lane];
+        const double gall = fmax(__builtin_fma(-6.0, (double)(n - 1), sv), frozen);
+        bool drop = gall < (((lrms_bits >> ib) & 1u) ? -5.0 : -15.0);
+        int nn = n;
+        if (total - nl >= 0) {
+            nn = n + 1;
+            total -= nl;
+            drop |= nn >= maxMantBits;
         } else {
             drop = true;
         }
+        bits[ib][lane] = (uint8_t)nn;
         if (drop) {
-            if (b == b0) v0 = false;
-            if (b == b1) v1 = false;
-            frozen = fmax(frozen, after);
+            cur[ib][lane] = -INFINITY;
+            frozen = fmax(frozen, __builtin_fma(-6.0, (double)(nn - 1), sv));
+        } else {
+            cur[ib][lane] = __builtin_fma(-6.0, (double)nn, sv);
         }
     }
-    int back = 0;
-    if (n0 == 1) { back += nl0; n0 = 0; }
-    if (has1 && n1 == 1) { back += nl1; n1 = 0; }
-    total += row_sum_i(back);
-    *ba0 = n0;
-    *ba1 = n1;
-    return total - extra;
+    int back = 0;                                      // bits[bits == 1] = 0, their lines back
+#pragma unroll
+    for (int b = 0; b < PAC_NB; ++b) {
+        if (bits[b][lane] == 1) {
+            back += nl_s[b];
+            bits[b][lane] = 0;
+        }
+    }
+    return total + back - extra;
 }
 
-// 16 lanes (one DPP row) per stream of the chunk, four streams per wave: the
-// serial reservoir chain over the stream's blocks t0 .. t0+S-1 --
-// withdrawBits, the two BitAlloc calls with the extraBits carry
-// (codec.py:222-260), scale factors, StripSignBits + Huffman.encodeData's
-// length scoring of the 10 tables (Huffman.py:274-309), depositBits
-// (codec.py:111-124) -- and each channel-block's byte count.
-__global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict__ T,
-                                                    const PacHuffTables* __restrict__ H,
-                                                    PacMasterChunkBuf K, PacMasterFields F,
-                                                    const int64_t* __restrict__ blk_off, PacMasterChunk ck,
-                                                    int64_t* __restrict__ st_extra,
-                                                    int64_t* __restrict__ st_deposit, double bitBudget) {
-    __shared__ uint8_t ba_s[4][32], sf_s[4][32];
-    // a latency-bound chain sharing the SIMDs with the next chunk's threshold
-    // waves: issue ahead of them
-    __builtin_amdgcn_s_setprio(3);
+#ifndef PAC_TAIL_U
+#define PAC_TAIL_U 8      // lines per lane whose loads are in flight together
+#endif
+
+// One lane per stream of the chunk, 64 streams per wave: for the stream's
+// blocks t0 .. t0+S-1 in order -- withdrawBits (Huffman.py:363-371,
+// codec.py:229), per channel BitAlloc with the extraBits carry (codec.py:
+// 249-260), scale factors and vMantissa (quantize.py:148-342), StripSignBits
+// + Huffman.encodeData's table choice by total length (Huffman.py:274-309),
+// depositBits (codec.py:111-124) -- and each channel-block's byte count.  The
+// signed mantissa codes go to F.codes for k_master_pack.
+// LDS: launched with PAC_TAIL_LDS bytes of dynamic shared memory -- declared
+// statically, its 29 KB would cap the compiler's occupancy estimate at 5
+// one-wave workgroups per CU and it would then ignore the 5-waves-per-SIMD
+// register budget (96 VGPRs) that lets a tail wave sit beside 4 threshold
+// waves (104 VGPRs each) on a SIMD.
+#define PAC_TAIL_LDS (2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE + PAC_NB * 4)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_master_tail(
+    const PacTables* __restrict__ T, const uint32_t* __restrict__ hsc, PacMasterChunkBuf K, PacMasterFields F,
+    const int64_t* __restrict__ blk_off, PacMasterChunk ck, int64_t* __restrict__ st_extra,
+    int64_t* __restrict__ st_deposit, double bitBudget) {
+    extern __shared__ __attribute__((aligned(16))) char tail_lds[];
+    double (*cur_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds);
+    double (*smr_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds + PAC_NB * WAVE * 8);
+    uint8_t (*bits_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + 2 * PAC_NB * WAVE * 8);
+    uint8_t (*sf_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + 2 * PAC_NB * WAVE * 8 + PAC_NB * WAVE);
+    int* nl_s = reinterpret_cast<int*>(tail_lds + 2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE);
     const int lane = threadIdx.x;
-    const int r = lane >> 4, q = lane & 15;
-    const int sl = blockIdx.x * 4 + r;
+    if (lane < PAC_NB) nl_s[lane] = T->nlines[lane];
+    wave_sync();                                       // one wave per workgroup; afterwards lanes touch only their columns
+    const int sl = blockIdx.x * WAVE + lane;
+    if (sl >= ck.n_s) return;
     const int nch = ck.nch;
-    if (sl >= ck.n_s) return;                          // whole rows only
     const int s = ck.s_first + sl;
     const int64_t bb0 = blk_off[s];
     const int64_t len = blk_off[s + 1] - bb0;
     const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
     long extra = st_extra[s], deposit = st_deposit[s];
-    const int b0 = q, b1 = q + 16;
-    const bool has1 = b1 < PAC_NB;
-    int esc[PAC_NTAB];
-#pragma unroll
-    for (int tb = 0; tb < PAC_NTAB; ++tb) esc[tb] = H->esc_len[tb];
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
     for (int64_t t = ck.t0; t < t_end; ++t) {
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
         const int64_t gb = bb0 + t;
@@ -894,79 +900,82 @@ __global__ __launch_bounds__(64) void k_master_tail(const PacTables* __restrict_
         if (deposit > 10) { e = deposit / 100; deposit -= e; }
         else if (deposit < 0) { e = deposit; deposit = 0; }
         extra += e;
+        uint32_t lrms_bits = 0;
+        for (int b = 0; b < PAC_NB; ++b) lrms_bits |= (uint32_t)(F.lrms[gb * PAC_NB + b] & 1) << b;
         long dep_add = 0;
         for (int ch = 0; ch < nch; ++ch) {
             const int64_t gl = j * 2 + ch, g = gb * nch + ch;
-            int a0, a1;
-            extra += bitalloc_master_row(K.smr + gl * PAC_NB, F.lrms + gb * PAC_NB, T, bitBudget, extra, 16, q,
-                                         &a0, &a1);
-            const int f0 = pac_scale_factor(K.bandpeak[gl * PAC_NB + b0], a0);
-            const int f1 = has1 ? pac_scale_factor(K.bandpeak[gl * PAC_NB + b1], a1) : 0;
-            ba_s[r][b0] = (uint8_t)a0;
-            sf_s[r][b0] = (uint8_t)f0;
-            F.ba[g * PAC_NB + b0] = (uint8_t)a0;
-            F.sf[g * PAC_NB + b0] = (uint8_t)f0;
-            if (has1) {
-                ba_s[r][b1] = (uint8_t)a1;
-                sf_s[r][b1] = (uint8_t)f1;
-                F.ba[g * PAC_NB + b1] = (uint8_t)a1;
-                F.sf[g * PAC_NB + b1] = (uint8_t)f1;
+            extra += bitalloc_lane(cur_s, smr_s, bits_s, nl_s, K.smr + gl * PAC_NB, lrms_bits, bitBudget, extra, 16,
+                                   lane);
+            // scale factors; the allocation's mantissa and sign bits
+            int orig = 0, nsign = 0;
+            for (int b = 0; b < PAC_NB; ++b) {
+                const int ba = bits_s[b][lane];
+                const int f = pac_scale_factor(K.bandpeak[gl * PAC_NB + b], ba);
+                sf_s[b][lane] = (uint8_t)f;
+                F.ba[g * PAC_NB + b] = (uint8_t)ba;
+                F.sf[g * PAC_NB + b] = (uint8_t)f;
+                orig += ba * nl_s[b];
+                nsign += ba ? nl_s[b] : 0;
             }
-            int nsign = (a0 ? T->nlines[b0] : 0) + (has1 && a1 ? T->nlines[b1] : 0);
-            int orig = a0 * T->nlines[b0] + (has1 ? a1 * T->nlines[b1] : 0);
-            wave_sync();
-            // Huffman scoring: lines l = 16 i + q of the 1024, eight at a time (one
-            // gather of the ten tables' lengths per line, the loads in flight together)
+            // mantissas (stored for the pack) and the ten tables' total lengths,
+            // PAC_TAIL_U lines at a time (their loads in flight together)
             const double* ln = K.lines + gl * PAC_HALFN;
             uint16_t* cs = F.codes + g * PAC_HALFN;
-            int acc[PAC_NTAB];
+            uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
+            for (int l0 = 0; l0 < lend; l0 += PAC_TAIL_U) {
+                double x[PAC_TAIL_U];
+                int bal[PAC_TAIL_U], sfl[PAC_TAIL_U];
 #pragma unroll
-            for (int tb = 0; tb < PAC_NTAB; ++tb) acc[tb] = 0;
-            for (int l0 = q; l0 < PAC_HALFN; l0 += 16 * 8) {
-                uint64_t lens[8];
-                int bal[8];
+                for (int u = 0; u < PAC_TAIL_U; ++u) {
+                    const int l = l0 + u;
+                    const int b = T->band_of_line[l];          // uniform
+                    bal[u] = l < lend ? bits_s[b][lane] : 0;
+                    sfl[u] = sf_s[b][lane];
+                    x[u] = bal[u] ? ln[l] : 0.0;
+                }
+                uint32_t m[PAC_TAIL_U];
+                const uint32_t* ent[PAC_TAIL_U];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int l = l0 + 16 * u;
-                    const int b = T->band_of_line[l];
-                    const int ba = ba_s[r][b];
-                    bal[u] = ba;
-                    lens[u] = 0;
-                    uint32_t m = 0;
-                    if (ba) {
-                        m = pac_mantissa(ln[l], sf_s[r][b], ba);
-                        lens[u] = H->lens10[m & ((1u << (ba - 1)) - 1u)];
+                for (int u = 0; u < PAC_TAIL_U; ++u) {
+                    m[u] = 0u;
+                    ent[u] = hsc;
+                    if (bal[u]) {
+                        const int ba = bal[u];
+                        m[u] = pac_mantissa(x[u], sfl[u], ba);
+                        ent[u] = hsc + (int64_t)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) * PAC_HSC_W;
                     }
-                    cs[l] = (uint16_t)m;          // the pack kernel's input
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (!bal[u]) continue;
-#pragma unroll
-                    for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                        const int L = (int)((lens[u] >> (5 * tb)) & 31u);
-                        acc[tb] += L ? L : esc[tb] + bal[u];
+                for (int u = 0; u < PAC_TAIL_U; ++u) {
+                    if (bal[u]) {
+                        const uint2 a = *reinterpret_cast<const uint2*>(ent[u]);
+                        const uint2 b2 = *reinterpret_cast<const uint2*>(ent[u] + 2);
+                        const uint32_t c4 = ent[u][4];
+                        acc[0] += a.x; acc[1] += a.y; acc[2] += b2.x; acc[3] += b2.y; acc[4] += c4;
                     }
+                }
+#pragma unroll
+                for (int u = 0; u < PAC_TAIL_U; u += 4) {      // four codes per 8-byte store
+                    const uint64_t w = (uint64_t)m[u] | ((uint64_t)m[u + 1] << 16) | ((uint64_t)m[u + 2] << 32) |
+                                       ((uint64_t)m[u + 3] << 48);
+                    *reinterpret_cast<uint64_t*>(cs + l0 + u) = w;
                 }
             }
-            nsign = row_sum_i(nsign);
-            orig = row_sum_i(orig);
             int best = 0, bestid = 1;
 #pragma unroll
             for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                const int v = row_sum_i(acc[tb]);
+                const int v = (int)((acc[tb >> 1] >> (16 * (tb & 1))) & 0xffffu);
                 if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
             }
             dep_add += (long)orig - ((long)best + nsign + 4);
-            if (q == 0) {
-                F.tid[g] = (uint8_t)bestid;
-                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
-            }
-            wave_sync();                               // ba_s / sf_s rewritten by the next channel
+            F.tid[g] = (uint8_t)bestid;
+            F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
         }
         deposit += dep_add;     // depositBits per channel (codec.py:120)
     }
-    if (q == 0) { st_extra[s] = extra; st_deposit[s] = deposit; }
+    st_extra[s] = extra;
+    st_deposit[s] = deposit;
 }
 
 // worst-case master channel-block: 8 + 25 * 8 + 25 (+ 1 block-switching) bits

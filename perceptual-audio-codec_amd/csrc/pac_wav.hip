@@ -71,7 +71,16 @@ __global__ void k_wav_scan(const uint8_t* __restrict__ blob, const int64_t* __re
     w.num_samples = (int64_t)(rd_u32(p + pos) / (nch * 2u));
     w.data_offset = pos + 4;
     w.frames = w.num_samples;
-    if (w.num_samples % hop == 0) {                  // the extra hop after the data (pacfile.py:240-242)
+    // ReadDataBlock stops at the first hop whose read comes back empty
+    // (pcmfile.py:69-80, the driver's break at pacfile.py:482): a file that
+    // holds fewer data bytes than its header claims (cut short, or a streaming
+    // header's 0xFFFFFFFF) is coded up to its last byte, the partial hop
+    // zero-padded, and never gets the extra hop
+    const int64_t avail = len - w.data_offset > 0 ? len - w.data_offset : 0;
+    const int64_t have = (avail + nch * 2 - 1) / (nch * 2);   // frames with at least one byte in the file
+    if (have < w.num_samples) {
+        w.frames = have;
+    } else if (w.num_samples % hop == 0) {           // the extra hop after the data (pacfile.py:240-242)
         const int64_t after = w.data_offset + w.num_samples * nch * 2;
         int64_t ex = len - after;
         ex = ex < 0 ? 0 : (ex > (int64_t)hop * nch * 2 ? (int64_t)hop * nch * 2 : ex);

@@ -199,6 +199,8 @@ def encode_wav_files(wav_files, profile=PROFILE_MASTER, context=None, n_channels
     blob = b"".join(blobs)
     if sample_rate is None or n_channels is None:
         first = ctx.wav_scan(blobs[0], [0, len(blobs[0])])[0]
+        if first.status:      # the reference's PCMFile raise for this file, not a parameter error
+            raise _lib.PacError(_lib.PAC_E_ARG, "file 0: " + _lib.wav_status_message(first.status))
         sample_rate = sample_rate or first.sample_rate
         n_channels = n_channels or first.n_channels
     p = _lib.params(sample_rate, n_channels, profile, window=window, block_switch=block_switch)

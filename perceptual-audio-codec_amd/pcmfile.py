@@ -119,14 +119,19 @@ def read_for_encode(path, nMDCTLines=1024):
     quirk (pacfile.py:240-242): when numSamples is an exact multiple of
     nMDCTLines the header count is bumped by nMDCTLines, and the reader then
     tries one more hop, which picks up whatever bytes follow the data chunk.
+    A file holding fewer data bytes than its header claims is read up to its
+    last byte (the partial frame zero-padded, as ReadDataBlock pads a short
+    read, pcmfile.py:73-78) and gets no extra hop: the next read comes back
+    empty and the driver stops (pacfile.py:482).
     """
     with open(path, "rb") as fp:
         nCh, fs, bits, ns = _scan_header(fp)
-        data_start = fp.tell()
         nbytes = ns * nCh * 2
         raw = fp.read(nbytes)
         extra = b""
-        if ns % nMDCTLines == 0:
+        if len(raw) < nbytes:
+            raw += b"\0" * (-len(raw) % (nCh * 2))
+        elif ns % nMDCTLines == 0:
             extra = fp.read(nMDCTLines * nCh * 2)
     frames = np.frombuffer(raw, dtype="<i2").reshape(-1, nCh)
     if extra:

@@ -11,8 +11,11 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-ARGS=${PROF_ARGS:-"--no-cpu --config 2 --streams 1000 --steps 2 --warmup 1"}
-TAG=${PROF_TAG:-r02_master}
+# default: the bench's own geometry (configs[2], 10^4 streams x 1000 blocks,
+# chunks of S = 6 blocks per stream), so the trace's per-kernel totals are
+# comparable with the bench line's kernels_ms
+ARGS=${PROF_ARGS:-"--no-cpu --config 2 --steps 2 --warmup 1"}
+TAG=${PROF_TAG:-r03_master}
 LIM=${PROF_LIMIT:-240}
 timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_kt -o kt -- python3 bench.py $ARGS > gpurun_out/prof_${TAG}_kt.log 2>&1 || { echo "kernel trace failed"; exit 1; }
 for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \

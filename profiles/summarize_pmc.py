@@ -85,8 +85,9 @@ def derive(c, blocks, total_ms):
         cyc = c["GRBM_GUI_ACTIVE"] / 8
         d["clock_ghz"] = cyc / (total_ms / 1e3) / 1e9
         d["valu_issue_util"] = c["SQ_INSTS_VALU"] * 4 / (SIMDS * cyc)
-    if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_ACTIVE_INST_LDS"):
-        d["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_ACTIVE_INST_LDS"]
+    if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+        # extra cycles / all LDS-array cycles (MI355X_MICROARCH.md LDS section)
+        d["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
     if "SQ_WAIT_ANY" in c and c.get("SQ_WAVE_CYCLES"):
         d["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
     return d

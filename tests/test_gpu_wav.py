@@ -72,6 +72,37 @@ def test_exact_multiple_quirk(ctx, tmp_path, tail, prof):
     assert got[len(pacfile.header_bytes(44100, 2, cp.numSamples)):] == exp
 
 
+@pytest.mark.parametrize("claimed,cut", [(3 * 1024 + 5, 2 * 4096 + 6), (4 * 1024, 3 * 4096 + 1),
+                                         (0xFFFFFFFF // 4, 5 * 4096 + 40), (4 * 1024, 0)])
+@pytest.mark.parametrize("prof", [pacfile.PROFILE_ORIGIN, pacfile.PROFILE_MASTER])
+def test_truncated_wav(ctx, tmp_path, claimed, cut, prof):
+    """data chunk shorter than its header (cut short, or a streaming header):
+    the device scan codes the bytes present, as the reference's reads
+    (pcmfile.py:69-80) -- equal to the host mirror and the oracle"""
+    pcm = synth.pink_tones_pcm(6 * 1024, 44100, seed=cut)
+    d = np.ascontiguousarray(pcm, dtype="<i2").tobytes()[:cut]
+    w = struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + len(d), b"WAVE", b"fmt ", 16, 1, 2, 44100, 44100 * 4, 4,
+                    16, b"data", min(claimed * 4, 0xFFFFFFFF)) + d
+    path = tmp_path / "t.wav"
+    path.write_bytes(w)
+    info = ctx.wav_scan(w, [0, len(w)])[0]
+    cp, fr = read_for_encode(str(path))
+    assert info.frames == fr.shape[0] == (cut + 3) // 4
+    got = pacfile.encode_wav_files([w], prof, context=ctx)[0]
+    assert got == pacfile.encode_file(str(path), profile=prof, context=ctx)
+    o = P.Oracle(44100, huffman=(prof == pacfile.PROFILE_MASTER))
+    exp = o.encode_data(P.MASTER if prof == pacfile.PROFILE_MASTER else P.ORIGIN, fr)
+    assert got[len(pacfile.header_bytes(44100, 2, cp.numSamples)):] == exp
+
+
+def test_bad_first_wav_raises_its_wav_error(ctx):
+    """sample rate and channels taken from the first file: a malformed first
+    file raises the reference's PCMFile error, not a parameter error"""
+    with pytest.raises(_lib.PacError) as e:
+        pacfile.encode_wav_files([b"RIFF0000WAVEjunkjunk"], pacfile.PROFILE_MASTER, context=ctx)
+    assert "'fmt '" in str(e.value)
+
+
 def test_bad_wav_raises(ctx):
     with pytest.raises(_lib.PacError) as e:
         pacfile.encode_wav_files([b"RIFX0000WAVEfmt "], pacfile.PROFILE_ORIGIN, context=ctx, n_channels=2,

@@ -112,6 +112,45 @@ def test_pcmfile_hop_reads_equal_bulk(tmp_path):
     assert np.all(np.concatenate(hops)[frames.shape[0]:] == 0)
 
 
+def _hop_loop(path):
+    """the reference driver's reads: PCMFile.ReadDataBlock until None, with
+    PACFile.WriteFileHeader's bump of the shared numSamples (pacfile.py:240-242)"""
+    pf = pcmfile.PCMFile(str(path))
+    cp = pf.OpenForReading()
+    cp.nSamplesPerBlock = 1024
+    if cp.numSamples % 1024 == 0:
+        cp.numSamples += 1024
+    hops = []
+    while True:
+        blk = pf.ReadDataBlock(cp)
+        if blk is None:
+            break
+        hops.append(np.stack(blk, 1))
+    pf.Close(cp)
+    return hops
+
+
+@pytest.mark.parametrize("claimed", [3 * 1024 + 5, 4 * 1024, 0xFFFFFFFF // 4])
+@pytest.mark.parametrize("cut", [0, 1, 3, 4 * 1024 + 2, 2 * 4096, 3 * 4096 + 7])
+def test_truncated_wav_reads_to_last_byte(tmp_path, claimed, cut):
+    """a data chunk cut short (or a streaming header's 0xFFFFFFFF): the reads
+    stop at the first empty hop, the partial one zero-padded, no extra hop --
+    read_for_encode == the hop loop"""
+    pcm = synth.white_pcm(4 * 1024, 2, seed=cut)
+    d = pcm.astype("<i2").tobytes()[:cut]
+    p = tmp_path / "t.wav"
+    p.write_bytes(struct.pack("<4sL4s4sLHHLLHH4sL", b"RIFF", 36 + len(d), b"WAVE", b"fmt ", 16, 1, 2,
+                              48000, 48000 * 4, 4, 16, b"data", min(claimed * 4, 0xFFFFFFFF)) + d)
+    hops = _hop_loop(p)
+    _, frames = pcmfile.read_for_encode(str(p))
+    assert frames.shape[0] == (cut + 3) // 4
+    assert len(hops) == (frames.shape[0] + 1023) // 1024
+    if hops:
+        whole = np.concatenate(hops)
+        assert np.array_equal(whole[: frames.shape[0]], pcmfile.codes_to_float(frames))
+        assert np.all(whole[frames.shape[0]:] == 0)
+
+
 def test_exact_multiple_reads_trailing_chunk(tmp_path):
     """numSamples % 1024 == 0: the bumped header count makes the reference
     reader take one more hop from the bytes after the data chunk."""

@@ -181,7 +181,8 @@ KERNEL_IO_BYTES = {
     "k_master_thr": 2 * 1025 * 16 + 6 * 1024 * 8,    # the spectra in; 6 threshold rows out (calcBTHR x 6)
     "k_master_front": 4096 + 6 * 1024 * 8 + 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2,
     "k_master_tail": 2 * 1024 * 8 + 4 * 25 * 8 + 25 + 2 * (25 * 2 + 1 + 4 + 8),
-    "k_master_pack": 2 * 1024 * 8 + 2 * 25 * 2 + 25 + 2 + 2 * 300,
+    "k_master_emit": 2 * 1024 * 2 + 2 * (25 * 2 + 1 + 4 + 8) + 25 + 2 * 300,   # codes + fields in; staged bytes out
+    "k_master_place": 2 * 2 * (300 + 8 + 4),                                     # staged bytes in, file bytes out
 }
 
 
@@ -513,8 +514,8 @@ PHASES = {  # pac_timing field -> kernel, per profile (include/pac_gpu.h)
                ("pack_ms", "k_origin_pack")],
     "master": [("lrms_ms", "k_master_lrms"), ("spec_ms", "k_master_spec"), ("thr_ms", "k_master_thr"),
                ("front_ms", "k_master_front"),
-               ("alloc_ms", "k_master_tail"),
-               ("pack_ms", "k_master_pack"), ("scan_ms", "k_scan")],
+               ("alloc_ms", "k_master_tail"), ("emit_ms", "k_master_emit"),
+               ("pack_ms", "k_master_place"), ("scan_ms", "k_scan")],
 }
 PHASES["bs"] = PHASES["master"] + [("thr_short_ms", "k_master_thr_short")]
 
@@ -567,12 +568,12 @@ def main():
     kern_ms = {k: float(np.mean([p[f] for p in per])) for f, k in PHASES["bs" if a.bs else a.profile]}
     # the dominant kernel on the critical path (the master reservoir tail runs on
     # a second stream, overlapped with the next chunk's thresholds)
-    dom = max((k for k in kern_ms if k != "k_master_tail"), key=kern_ms.get)
+    dom = max((k for k in kern_ms if k not in ("k_master_tail", "k_master_emit")), key=kern_ms.get)
     dom_s = kern_ms[dom] / 1e3
     step_s = el_max / a.steps
     # algorithmic bytes = PCM read + bitstream written, per block
     alg_per_block = PCM_BYTES_PER_BLOCK + out_bytes / blocks
-    launches = sum(master_launches(j.bcounts) for j in jobs) if a.master and dom != "k_master_pack" else len(jobs)
+    launches = sum(master_launches(j.bcounts) for j in jobs) if a.master and dom != "k_master_place" else len(jobs)
     achieved = alg_per_block * blocks / dom_s / 1e9 if dom_s > 0 else 0.0
     prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
     traffic_pb = None

@@ -103,6 +103,8 @@ typedef struct {
     float lrms_ms;
     float thr_short_ms; /* block switching: k_master_thr_short (the short frames' thresholds) */
     float spec_ms;      /* master: k_master_spec (the windowed L/R spectra the thresholds derive from) */
+    float emit_ms;      /* master: k_master_emit (the bitstream packing beside the next chunk's tail; pack_ms
+                           is then k_master_place, the copy to the file offsets) */
 } pac_timing;
 
 /* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */

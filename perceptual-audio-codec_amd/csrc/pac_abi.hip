@@ -323,7 +323,12 @@ struct pac_ctx {
     DevBuf<double2> m_spec;               // [chunk][2][PAC_SPEC_LD] k_master_spec -> k_master_thr
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
     DevBuf<uint32_t> m_rowm;                // [nblocks] k_master_lrms -> k_master_thr row masks
-    DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack)
+    DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack; pack path only)
+    DevBuf<uint16_t> m_ccodes;              // master: the chunk's codes, tail-internal (emission path)
+    DevBuf<uint8_t> m_stg;                  // master: channel-blocks emitted by the tail (staging)
+    DevBuf<int64_t> m_stoff;                // master: staging offset per channel-block
+    DevBuf<unsigned long long> m_stg_next;  // master: staging bump allocator
+    DevBuf<uint64_t> hcode;                 // [10][PAC_NSYM] (code length << 32) | code bits, 0: escape
     DevBuf<int64_t> st_extra, st_deposit;
     DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
     DevBuf<uint64_t> dbg_code;
@@ -331,16 +336,13 @@ struct pac_ctx {
     DevBuf<uint8_t> bs_att, bs_fl;          // block switching: attack / PAC_BS_* flags per block
     DevBuf<uint8_t> dec_bsf;                // decoder: the short-frame bit per channel-block
     hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
-    hipStream_t stream3 = nullptr;          // master: the LRMS decisions, running ahead of the thresholds
-    // PAC_LRMS_ASYNC=1: LRMS on its own stream, running ahead of the thresholds.
-    // Off by default: since k_master_lrms fits 5 workgroups per CU the overlap
-    // no longer gains (3.71 vs 3.72 M blocks/s) and in line every kernel's
-    // event time is its own (clean per-kernel rooflines)
-    bool lrms_async = false;
-    // PAC_TAIL_MODE=serial: the reservoir tail of each chunk on `stream`
-    // right after the chunk's front kernels (nothing co-runs) -- the
-    // measurement baseline of the default placement (run_master)
+    hipStream_t stream3 = nullptr;          // master: the next chunk's LRMS decisions and spectra
+    hipStream_t stream4 = nullptr;          // master: the bitstream emission of the previous chunk
+    // PAC_TAIL_MODE=serial: every master kernel on `stream` in order (nothing
+    // co-runs) -- the measurement baseline of run_master's pipelined placement
     bool tail_serial = false;
+    int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
+    int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
     // decoder
     DevBuf<uint32_t> hdec_tab;              // two-level Huffman decoding tables (device)
@@ -381,9 +383,12 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     pac_ctx* c = new pac_ctx();
     c->device = device;
     if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
+    if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
+    if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
                     hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess;
+                    hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess &&
+                    hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
@@ -391,7 +396,6 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     for (auto& e : c->ev) hipEventCreate(&e);
     for (auto& e : c->evs) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (const char* f = getenv("PAC_DEBUG_FLAGS")) c->dbg = atoi(f);
-    if (const char* f = getenv("PAC_LRMS_ASYNC")) c->lrms_async = atoi(f) != 0;
     *out = c;
     return PAC_OK;
 }
@@ -402,8 +406,10 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->stream2);
     hipStreamSynchronize(c->stream3);
+    hipStreamSynchronize(c->stream4);
     for (auto& kv : c->tables) hipFree(kv.second);
-    c->hscore.release();
+    c->hscore.release(); c->hcode.release(); c->m_ccodes.release(); c->m_stg.release(); c->m_stoff.release();
+    c->m_stg_next.release();
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
@@ -426,6 +432,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamDestroy(c->stream);
     hipStreamDestroy(c->stream2);
     hipStreamDestroy(c->stream3);
+    hipStreamDestroy(c->stream4);
     delete c;
 }
 
@@ -516,6 +523,15 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
     if (hipMemcpy(c->hscore.p, hs.data(), hs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
         free(h);
         return set_err(PAC_E_HIP, "huffman scoring table upload");
+    }
+    std::vector<uint64_t> hc((size_t)PAC_NTAB * PAC_NSYM, 0ull);
+    for (int t = 0; t < PAC_NTAB; t++)
+        for (int sym = 0; sym < PAC_NSYM; sym++)
+            if (h->len[t][sym]) hc[(size_t)t * PAC_NSYM + sym] = ((uint64_t)h->len[t][sym] << 32) | h->bits[t][sym];
+    if ((rc3 = c->hcode.ensure(hc.size()))) { free(h); return rc3; }
+    if (hipMemcpy(c->hcode.p, hc.data(), hc.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+        free(h);
+        return set_err(PAC_E_HIP, "huffman code table upload");
     }
     if (!c->huff && hipMalloc((void**)&c->huff, sizeof(PacHuffTables)) != hipSuccess) {
         free(h);
@@ -747,6 +763,7 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
     c->last.lrms_ms = 0.f;
     c->last.thr_short_ms = 0.f;
     c->last.spec_ms = 0.f;
+    c->last.emit_ms = 0.f;
     hipEventSynchronize(c->ev[4]);
     hipEventElapsedTime(&c->last.front_ms, c->ev[0], c->ev[1]);
     hipEventElapsedTime(&c->last.alloc_ms, c->ev[1], c->ev[2]);
@@ -770,9 +787,16 @@ static void finish_timing(pac_ctx* c, int64_t G, int64_t bytes) {
 // final offsets, then k_master_pack writes every channel-block in place.
 // No host synchronisation inside the pipeline.  Leaves the offsets in c->off
 // and the total (async) in *out_total.
+// pack = false: the tail emits every channel-block into the staging buffer
+// and k_master_place copies them to their offsets; *stg_need (host, async)
+// receives the staging bytes it used -- more than *stg_cap means some were
+// not emitted and the caller re-runs with pack = true.  pack = true (and the
+// per-block API's debug codes): the tail stores the mantissa codes of every
+// channel-block and k_master_pack packs them.
 static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource src,
                       const std::vector<int64_t>& blk, uint8_t* out_dev, int64_t out_cap,
-                      int64_t* out_total, bool dbg_codes) {
+                      int64_t* out_total, bool dbg_codes, bool pack = true, uint64_t* stg_need = nullptr,
+                      int64_t* stg_cap = nullptr) {
     int rc;
     const int n_streams = src.n_streams;
     const int64_t nblocks = blk[n_streams];
@@ -798,12 +822,33 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(2 * cbmax * 2 * PAC_HALFN)) ||
-        (rc = c->m_smr.ensure(2 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(2 * cbmax * 2 * PAC_NB)))
+        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_smr.ensure(3 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(3 * cbmax * 2 * PAC_NB)))
         return rc;
-    if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
+    pack = pack || dbg_codes;
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
-                      nullptr, nullptr, nullptr, c->m_codes.p, nullptr, c->m_rowm.p};
+                      nullptr, nullptr, nullptr, nullptr, nullptr, c->m_rowm.p, nullptr, nullptr, nullptr, 0};
+    if (pack) {
+        if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
+        F.codes = c->m_codes.p;
+    } else {
+        // staging: the output's capacity (at most a 1.5 KB average per
+        // channel-block -- the bit budget gives ~300 B) + 4 B of alignment
+        // padding per channel-block; a larger need is detected after the call
+        int64_t cap = std::min<int64_t>(out_cap, G * 1536) + 4 * G + 64 + c->stg_bias;
+        if (c->stg_cap_max > 0) cap = std::min<int64_t>(cap, c->stg_bias + c->stg_cap_max);
+        if ((rc = c->m_ccodes.ensure(2 * cbmax * 2 * PAC_HALFN)) || (rc = c->m_stg.ensure(cap)) ||
+            (rc = c->m_stoff.ensure(G + 1)) || (rc = c->m_stg_next.ensure(1)))
+            return rc;
+        F.stg = c->m_stg.p;
+        F.stoff = c->m_stoff.p;
+        F.stg_next = c->m_stg_next.p;
+        F.stg_cap = cap;
+        const unsigned long long bias = (unsigned long long)c->stg_bias;
+        HIPCHK(hipMemcpyAsync(c->m_stg_next.p, &bias, sizeof(bias), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));   // `bias` is a stack value
+        if (stg_cap) *stg_cap = cap;
+    }
     if (p->block_switch) {     // pac_bs.h: attack flags, then each block's PAC_BS_* flags
         if ((rc = c->bs_att.ensure(nblocks + 1)) || (rc = c->bs_fl.ensure(nblocks + 1))) return rc;
         hipLaunchKernelGGL(k_bs_attack, dim3((unsigned)((nblocks + 1) / 2)), dim3(64), 0, c->stream, src, nblocks,
@@ -821,101 +866,120 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         F.dbg_code = c->dbg_code.p;
         F.dbg_len = c->dbg_len.p;
     }
-    hipStream_t s0 = c->stream, s1 = c->tail_serial ? c->stream : c->stream2, s2 = c->stream3;
-    const bool lrms_async = c->lrms_async && nch == 2;
+    // Streams: s0 the thresholds and the front (the critical path), s2 the
+    // LRMS decisions and spectra of the NEXT chunk, s1 the reservoir tail.
+    // Per chunk i (buffer set k = i % 3 of the front -> tail outputs):
+    //   s0: thr(i) -> front(i) -> [wait spec(i+1)] -> thr(i+1) ...
+    //   s2: [wait thr(i): the spectrum buffer is free] lrms(i+1) -> spec(i+1)
+    //   s1: [wait front(i), spec(i+1)] tail(i), beside thr(i+1)
+    // lrms/spec of the next chunk thus co-run with front(i) (three
+    // latency-bound kernels filling each other's issue gaps), and the tail
+    // (<= 96 VGPRs, one wave per workgroup) takes the fifth wave slot of a
+    // SIMD next to 4 threshold waves (104 VGPRs each) without displacing one.
+    // PAC_TAIL_MODE=serial: every kernel on s0 in order (the baseline).
+    const bool serial = c->tail_serial;
+    hipStream_t s0 = c->stream, s1 = serial ? c->stream : c->stream2, s2 = serial ? c->stream : c->stream3;
+    hipStream_t s3 = serial ? c->stream : c->stream4;
     const double budget = bit_budget(p);
     // timing: events recorded around every launch on its own stream, read
     // once after the call; mk[k] = (pool event, phase) of stream k, phase -1
     // opens an interval, phase >= 0 closes one
-    std::vector<std::pair<size_t, int>> mk[3];
+    std::vector<std::pair<size_t, int>> mk[4];
     size_t nev = 0;
     auto mark = [&](int k, int phase) -> int {
         if (!c->timing) return PAC_OK;
         const hipEvent_t e = c->pool_event(nev);
         mk[k].emplace_back(nev++, phase);
-        HIPCHK(hipEventRecord(e, k == 2 ? s2 : (k ? s1 : s0)));
+        HIPCHK(hipEventRecord(e, k == 3 ? s3 : k == 2 ? s2 : (k ? s1 : s0)));
         return PAC_OK;
+    };
+    auto event_on = [&](hipStream_t st) -> hipEvent_t {   // a fresh ordering event (no timing)
+        const hipEvent_t e = c->pool_event(nev++);
+        hipEventRecord(e, st);
+        return e;
     };
     // mono: the LRMS flags are all 0 (L/R coding; the 25 bits are still written)
     if (nch == 1) HIPCHK(hipMemsetAsync(c->m_lrms.p, 0, nblocks * PAC_NB, s0));
-    HIPCHK(hipEventRecord(c->evs[4], s0));            // states and tables are on s0
-    HIPCHK(hipStreamWaitEvent(s1, c->evs[4], 0));
-    if (lrms_async) HIPCHK(hipStreamWaitEvent(s2, c->evs[4], 0));
-    // The tail of chunk i runs on s1 once chunk i+1's spectra are done, i.e.
-    // next to chunk i+1's threshold kernel: k_master_thr holds 4 waves per
-    // SIMD (104 of 512 VGPRs each) and the tail (<= 96 VGPRs, one wave per
-    // workgroup, 256 B of LDS) fills the fifth slot without displacing a
-    // threshold workgroup.  Launched right after chunk i's front instead, it
-    // shares the CUs with chunk i+1's LRMS kernel (5 workgroups per CU), which
-    // then runs at half speed.
-    struct Pend { PacMasterChunk ck; PacMasterChunkBuf K; int k, n_s; };
-    std::vector<Pend> pend;
-    auto launch_tail = [&](const Pend& t) -> int {
+    {
+        const hipEvent_t e = event_on(s0);            // states and tables are on s0
+        HIPCHK(hipStreamWaitEvent(s1, e, 0));
+        HIPCHK(hipStreamWaitEvent(s2, e, 0));
+        HIPCHK(hipStreamWaitEvent(s3, e, 0));
+    }
+    struct Chunk { PacMasterChunk ck; int64_t B; int n_s; };
+    std::vector<Chunk> chunks;
+    for (const Grp& gr : groups)
+        for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S)
+            chunks.push_back({PacMasterChunk{gr.g0, gr.n_s, t0, gr.S, nch}, (int64_t)gr.n_s * gr.S, gr.n_s});
+    const int64_t nck = (int64_t)chunks.size();
+    auto bufset = [&](int64_t i) {
+        const int64_t k = i % 3;
+        return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
+                                 c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
+                                 c->m_spec.p, c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN};
+    };
+    auto launch_side = [&](int64_t i) -> int {         // lrms(i), spec(i) on s2
         int rc2;
-        HIPCHK(hipEventRecord(c->evs[t.k], s0));
-        HIPCHK(hipStreamWaitEvent(s1, c->evs[t.k], 0));
-        if ((rc2 = mark(1, -1))) return rc2;
-        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((t.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS, s1, T,
-                           c->hscore.p, t.K, F,
-                           c->blk_off.p, t.ck, c->st_extra.p, c->st_deposit.p, budget);
+        const Chunk& q = chunks[i];
+        const PacMasterChunkBuf K = bufset(i);
+        if ((rc2 = mark(2, -1))) return rc2;
+        if (nch == 2) hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)q.B), dim3(256), 0, s2, src, T, F, q.ck);
+        if ((rc2 = mark(2, 5))) return rc2;
+        hipLaunchKernelGGL(k_master_spec, dim3((unsigned)q.B), dim3(256), 0, s2, src, T, K, F, q.ck);
         HIPCHK(hipGetLastError());
-        if ((rc2 = mark(1, 2))) return rc2;
-        HIPCHK(hipEventRecord(c->evs[2 + t.k], s1));
+        if ((rc2 = mark(2, 7))) return rc2;
         return PAC_OK;
     };
-    int64_t i = 0;
-    for (const Grp& gr : groups) {
-        for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S, ++i) {
-            const int k = (int)(i & 1);
-            const PacMasterChunk ck{gr.g0, gr.n_s, t0, gr.S, nch};
-            const PacMasterChunkBuf K{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
-                                      c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
-                                      c->m_spec.p};
-            const int64_t B = (int64_t)gr.n_s * gr.S;
-            if (i >= 2) HIPCHK(hipStreamWaitEvent(s0, c->evs[2 + k], 0));   // tail(i-2) done with set k
-            if (lrms_async) {
-                // the LRMS decisions depend on the PCM alone: on their own stream,
-                // free to run ahead and fill the issue slots the thresholds leave
-                if ((rc = mark(2, -1))) return rc;
-                hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s2, src, T, F, ck);
-                if ((rc = mark(2, 5))) return rc;
-                const hipEvent_t ev = c->pool_event(nev++);
-                HIPCHK(hipEventRecord(ev, s2));
-                HIPCHK(hipStreamWaitEvent(s0, ev, 0));
-                if ((rc = mark(0, -1))) return rc;
-            } else {
-                if ((rc = mark(0, -1))) return rc;
-                if (nch == 2)
-                    hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)B), dim3(256), 0, s0, src, T, F, ck);
-                if ((rc = mark(0, 5))) return rc;
-            }
-            hipLaunchKernelGGL(k_master_spec, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
-            if ((rc = mark(0, 7))) return rc;
-            if (!pend.empty()) {                  // the previous chunk's tail, next to this chunk's thresholds
-                if ((rc = launch_tail(pend.back()))) return rc;
-                pend.clear();
-            }
-            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
-                               T, K, F, ck);
-            if ((rc = mark(0, 0))) return rc;
-            if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
-                hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(B * nvar)), dim3(256), 0, s0, src, T, K, F,
-                                   ck);
-                if ((rc = mark(0, 6))) return rc;
-            }
-            hipLaunchKernelGGL(k_master_front, dim3((unsigned)B), dim3(256), 0, s0, src, T, K, F, ck);
+    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr);
+    if ((rc = launch_side(0))) return rc;
+    hipEvent_t spec_ready = event_on(s2);
+    for (int64_t i = 0; i < nck; ++i) {
+        const Chunk& q = chunks[i];
+        const PacMasterChunkBuf K = bufset(i);
+        HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
+        if (i >= 3) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
+        if ((rc = mark(0, -1))) return rc;
+        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
+                           T, K, F, q.ck);
+        if ((rc = mark(0, 0))) return rc;
+        if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
+            hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(q.B * nvar)), dim3(256), 0, s0, src, T, K, F,
+                               q.ck);
+            if ((rc = mark(0, 6))) return rc;
+        }
+        const hipEvent_t thr_done = event_on(s0);
+        if (i + 1 < nck) {                            // the next chunk's LRMS + spectra, beside this front
+            HIPCHK(hipStreamWaitEvent(s2, thr_done, 0));
+            if ((rc = launch_side(i + 1))) return rc;
+            spec_ready = event_on(s2);
+        }
+        if ((rc = mark(0, -1))) return rc;
+        hipLaunchKernelGGL(k_master_front, dim3((unsigned)q.B), dim3(256), 0, s0, src, T, K, F, q.ck);
+        HIPCHK(hipGetLastError());
+        if ((rc = mark(0, 1))) return rc;
+        // the tail of this chunk once the next chunk's spectra are ready too,
+        // i.e. beside the next chunk's thresholds
+        HIPCHK(hipStreamWaitEvent(s1, event_on(s0), 0));
+        if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, spec_ready, 0));
+        if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
+        if ((rc = mark(1, -1))) return rc;
+        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((q.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS, s1,
+                           T, c->hscore.p, K, F, c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
+        HIPCHK(hipGetLastError());
+        if ((rc = mark(1, 2))) return rc;
+        tail_done[i] = event_on(s1);
+        if (!pack) {                                  // this chunk's bitstream, beside the next chunk's tail
+            HIPCHK(hipStreamWaitEvent(s3, tail_done[i], 0));
+            if ((rc = mark(3, -1))) return rc;
+            hipLaunchKernelGGL(k_master_emit, dim3((unsigned)((q.B * nch + WAVE - 1) / WAVE)), dim3(WAVE), 0, s3, T,
+                               c->huff, c->hcode.p, K, F, c->blk_off.p, q.ck);
             HIPCHK(hipGetLastError());
-            if ((rc = mark(0, 1))) return rc;
-            pend.push_back({ck, K, k, gr.n_s});
-            if (c->tail_serial) {
-                if ((rc = launch_tail(pend.back()))) return rc;
-                pend.clear();
-            }
+            if ((rc = mark(3, 8))) return rc;
+            emit_done[i] = event_on(s3);
         }
     }
-    if (!pend.empty() && (rc = launch_tail(pend.back()))) return rc;
-    HIPCHK(hipEventRecord(c->evs[4], s1));
-    HIPCHK(hipStreamWaitEvent(s0, c->evs[4], 0));
+    HIPCHK(hipStreamWaitEvent(s0, event_on(s1), 0));
+    HIPCHK(hipStreamWaitEvent(s0, event_on(s3), 0));
     // pass 2: byte offsets in file order, then the packing
     if ((rc = mark(0, -1))) return rc;
     const int64_t ntiles = (G + SCAN_TILE - 1) / SCAN_TILE;
@@ -925,15 +989,21 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                        c->off.p);
     HIPCHK(hipGetLastError());
     if ((rc = mark(0, 4))) return rc;
-    hipLaunchKernelGGL(k_master_pack, dim3((unsigned)nblocks), dim3(256), 0, s0, T, c->huff, F, nch, nblocks,
-                       c->off.p, out_dev, out_cap);
+    if (pack) {
+        hipLaunchKernelGGL(k_master_pack, dim3((unsigned)nblocks), dim3(256), 0, s0, T, c->huff, F, nch, nblocks,
+                           c->off.p, out_dev, out_cap);
+    } else {
+        hipLaunchKernelGGL(k_master_place, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, s0, F, G, c->off.p, out_dev,
+                           out_cap);
+        if (stg_need) HIPCHK(hipMemcpyAsync(stg_need, c->m_stg_next.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s0));
+    }
     HIPCHK(hipGetLastError());
     if ((rc = mark(0, 3))) return rc;
     HIPCHK(hipMemcpyAsync(out_total, c->grand_total.p, sizeof(int64_t), hipMemcpyDeviceToHost, s0));
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
-        float ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = 0; k < 3; k++)
+        float ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < 4; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
                 float ms = 0.f;
@@ -948,6 +1018,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         c->last.lrms_ms = ph[5];
         c->last.thr_short_ms = ph[6];
         c->last.spec_ms = ph[7];
+        c->last.emit_ms = ph[8];
         c->last.total_ms = ph[0] + ph[1] + ph[3] + ph[4] + ph[5] + ph[6] + ph[7];   // the tail overlaps the next chunk
         c->last.n_channel_blocks = G;
         c->last.out_bytes = 0;
@@ -1036,7 +1107,15 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
             for (int i = 0; i < n_streams; i++) { ex[i] = states[i].extra_bits; dp[i] = states[i].bit_deposit; }
         HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false))) return rc;
+        uint64_t need = 0;
+        int64_t scap = 0;
+        if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false, false, &need, &scap))) return rc;
+        HIPCHK(hipStreamSynchronize(s));
+        if ((int64_t)need > scap) {   // the staging overflowed (> 1.5 KB per channel-block): again, packing
+            HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false, true))) return rc;
+        }
         hipLaunchKernelGGL(k_stream_offsets, dim3((n_streams + 1 + 255) / 256), dim3(256), 0, s, c->off.p,
                            c->blk_off.p, n_streams, nch, c->grand_total.p, c->stream_off.p);
         HIPCHK(hipGetLastError());

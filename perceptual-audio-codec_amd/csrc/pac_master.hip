@@ -26,19 +26,21 @@
 //   k_master_pack   one workgroup per block (pass 2): from the tail's stored
 //                   mantissa codes, sign bits, Huffman codes and LRMS packed
 //                   MSB-first (pacfile.py:288-351) straight to the final offset.
-// The tail of chunk i runs on a second HIP stream, concurrently with the
-// threshold/front kernels of chunk i+1 (double-buffered chunk outputs).
+// The LRMS + spectra of chunk i+1 run beside the front of chunk i, the tail of
+// chunk i beside the thresholds of chunk i+1 (three HIP streams, run_master).
 
 #include "pac_bs.h"
 
-// chunk-local scratch, local block j (thr single-buffered: written and read on
-// the front stream; the rest double-buffered between front and tail)
+// chunk-local scratch, local block j (thr and spec single-buffered, ordered by
+// events in run_master; lines / smr / bandpeak triple-buffered between the
+// front of chunk i and its tail, which runs beside chunk i+1's thresholds)
 struct PacMasterChunkBuf {
     double* thr;        // [Bc][6][1024]
     double* lines;      // [Bc][2][1024]  LRMSmdctLines
     double* smr;        // [Bc][2][25]
     double* bandpeak;   // [Bc][2][25]    max |line| per band
     double2* spec;      // [Bc][2][PAC_SPEC_LD] FFT bins -2..1026 of a and b (k_master_spec)
+    uint16_t* codes;    // [Bc][2][1024] signed mantissa codes, tail-internal (F.codes when the pack runs)
 };
 #define PAC_SPEC_LD 1040    // double2 per spectrum: bins -2..1026 at [bin + 2], padded to 256 B
 
@@ -58,6 +60,13 @@ struct PacMasterFields {
     uint16_t* codes;     // [G][1024] signed mantissa codes (tail -> pack; 0 where ba == 0)
     const uint8_t* bsf;  // [nblocks] PAC_BS_* flags (block-switching extension), or null: off
     uint32_t* rowm;      // [nblocks] 64-line rows of L/R-coded bands (bits 0-15), M/S-coded (16-31), k_master_lrms
+    // the tail's bitstream emission (null: k_master_pack packs from `codes`):
+    // each channel-block's '<L' nBytes + payload at stg + stoff[g] (4-byte
+    // aligned, padded to 4), placed at its file offset by k_master_place
+    uint8_t* stg;
+    int64_t* stoff;      // [G]
+    unsigned long long* stg_next;   // bump allocator of stg
+    int64_t stg_cap;
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of streams
@@ -857,19 +866,53 @@ __device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)
 #define PAC_TAIL_U 8      // lines per lane whose loads are in flight together
 #endif
 
-// One lane per stream of the chunk, 64 streams per wave: for the stream's
-// blocks t0 .. t0+S-1 in order -- withdrawBits (Huffman.py:363-371,
-// codec.py:229), per channel BitAlloc with the extraBits carry (codec.py:
-// 249-260), scale factors and vMantissa (quantize.py:148-342), StripSignBits
-// + Huffman.encodeData's table choice by total length (Huffman.py:274-309),
-// depositBits (codec.py:111-124) -- and each channel-block's byte count.  The
-// signed mantissa codes go to F.codes for k_master_pack.
+// exclusive prefix of an int across the wave by DPP; *total = the wave's sum
+__device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
+    int x = v;
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(1), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(2), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(4), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(8), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST15, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST31, 0xc, 0xf, false);
+    *total = __builtin_amdgcn_readlane(x, 63);
+    return x - v;
+}
+
+// MSB-first bit writer of one lane into 4-byte-aligned memory (big-endian
+// words: the bytes in file order)
+struct LaneBits {
+    uint32_t* w;
+    uint64_t acc;
+    int n;
+    __device__ __forceinline__ void put(uint32_t v, int bits) {    // bits <= 32, v < 2^bits
+        acc = (acc << bits) | v;
+        n += bits;
+        if (n >= 32) {
+            n -= 32;
+            *w++ = __builtin_bswap32((uint32_t)(acc >> n));
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        if (n > 0) *w = __builtin_bswap32((uint32_t)(acc << (32 - n)));
+    }
+};
+
 // LDS: launched with PAC_TAIL_LDS bytes of dynamic shared memory -- declared
 // statically, its 29 KB would cap the compiler's occupancy estimate at 5
 // one-wave workgroups per CU and it would then ignore the 5-waves-per-SIMD
 // register budget (96 VGPRs) that lets a tail wave sit beside 4 threshold
 // waves (104 VGPRs each) on a SIMD.
 #define PAC_TAIL_LDS (2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE + PAC_NB * 4)
+
+// One lane per stream of the chunk, 64 streams per wave: for the stream's
+// blocks t0 .. t0+S-1 in order -- withdrawBits (Huffman.py:363-371,
+// codec.py:229), per channel BitAlloc with the extraBits carry (codec.py:
+// 249-260), scale factors and vMantissa (quantize.py:148-342), StripSignBits
+// + Huffman.encodeData's table choice by total length (Huffman.py:274-309),
+// depositBits (codec.py:111-124) -- and each channel-block's byte count.
+// The signed mantissa codes go to the chunk's K.codes for k_master_emit, or
+// to F.codes for k_master_pack.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_master_tail(
     const PacTables* __restrict__ T, const uint32_t* __restrict__ hsc, PacMasterChunkBuf K, PacMasterFields F,
     const int64_t* __restrict__ blk_off, PacMasterChunk ck, int64_t* __restrict__ st_extra,
@@ -884,98 +927,222 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     if (lane < PAC_NB) nl_s[lane] = T->nlines[lane];
     wave_sync();                                       // one wave per workgroup; afterwards lanes touch only their columns
     const int sl = blockIdx.x * WAVE + lane;
-    if (sl >= ck.n_s) return;
+    const bool live = sl < ck.n_s;                     // every lane stays for the wave-wide steps
     const int nch = ck.nch;
-    const int s = ck.s_first + sl;
+    const int s = ck.s_first + (live ? sl : 0);
     const int64_t bb0 = blk_off[s];
     const int64_t len = blk_off[s + 1] - bb0;
-    const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
-    long extra = st_extra[s], deposit = st_deposit[s];
+    const int64_t t_end = !live ? ck.t0 : (ck.t0 + ck.S < len ? ck.t0 + ck.S : len);
+    long extra = live ? st_extra[s] : 0, deposit = live ? st_deposit[s] : 0;
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-    for (int64_t t = ck.t0; t < t_end; ++t) {
+    for (int64_t t = ck.t0; t < ck.t0 + ck.S; ++t) {   // wave-uniform trip count
+        const bool act = t < t_end;
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
         const int64_t gb = bb0 + t;
-        // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
-        long e = 0;
-        if (deposit > 10) { e = deposit / 100; deposit -= e; }
-        else if (deposit < 0) { e = deposit; deposit = 0; }
-        extra += e;
         uint32_t lrms_bits = 0;
-        for (int b = 0; b < PAC_NB; ++b) lrms_bits |= (uint32_t)(F.lrms[gb * PAC_NB + b] & 1) << b;
         long dep_add = 0;
+        if (act) {
+            // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
+            long e = 0;
+            if (deposit > 10) { e = deposit / 100; deposit -= e; }
+            else if (deposit < 0) { e = deposit; deposit = 0; }
+            extra += e;
+            for (int b = 0; b < PAC_NB; ++b) lrms_bits |= (uint32_t)(F.lrms[gb * PAC_NB + b] & 1) << b;
+        }
         for (int ch = 0; ch < nch; ++ch) {
             const int64_t gl = j * 2 + ch, g = gb * nch + ch;
-            extra += bitalloc_lane(cur_s, smr_s, bits_s, nl_s, K.smr + gl * PAC_NB, lrms_bits, bitBudget, extra, 16,
-                                   lane);
-            // scale factors; the allocation's mantissa and sign bits
-            int orig = 0, nsign = 0;
-            for (int b = 0; b < PAC_NB; ++b) {
-                const int ba = bits_s[b][lane];
-                const int f = pac_scale_factor(K.bandpeak[gl * PAC_NB + b], ba);
-                sf_s[b][lane] = (uint8_t)f;
-                F.ba[g * PAC_NB + b] = (uint8_t)ba;
-                F.sf[g * PAC_NB + b] = (uint8_t)f;
-                orig += ba * nl_s[b];
-                nsign += ba ? nl_s[b] : 0;
-            }
-            // mantissas (stored for the pack) and the ten tables' total lengths,
-            // PAC_TAIL_U lines at a time (their loads in flight together)
-            const double* ln = K.lines + gl * PAC_HALFN;
-            uint16_t* cs = F.codes + g * PAC_HALFN;
-            uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
-            for (int l0 = 0; l0 < lend; l0 += PAC_TAIL_U) {
-                double x[PAC_TAIL_U];
-                int bal[PAC_TAIL_U], sfl[PAC_TAIL_U];
-#pragma unroll
-                for (int u = 0; u < PAC_TAIL_U; ++u) {
-                    const int l = l0 + u;
-                    const int b = T->band_of_line[l];          // uniform
-                    bal[u] = l < lend ? bits_s[b][lane] : 0;
-                    sfl[u] = sf_s[b][lane];
-                    x[u] = bal[u] ? ln[l] : 0.0;
+            uint16_t* cs = F.codes ? F.codes + g * PAC_HALFN : K.codes + gl * PAC_HALFN;
+            int orig = 0, nsign = 0, best = 0, bestid = 1, nb = 0;
+            if (act) {
+                extra += bitalloc_lane(cur_s, smr_s, bits_s, nl_s, K.smr + gl * PAC_NB, lrms_bits, bitBudget, extra,
+                                       16, lane);
+                // scale factors; the allocation's mantissa and sign bits
+                for (int b = 0; b < PAC_NB; ++b) {
+                    const int ba = bits_s[b][lane];
+                    const int f = pac_scale_factor(K.bandpeak[gl * PAC_NB + b], ba);
+                    sf_s[b][lane] = (uint8_t)f;
+                    F.ba[g * PAC_NB + b] = (uint8_t)ba;
+                    F.sf[g * PAC_NB + b] = (uint8_t)f;
+                    orig += ba * nl_s[b];
+                    nsign += ba ? nl_s[b] : 0;
                 }
-                uint32_t m[PAC_TAIL_U];
-                const uint32_t* ent[PAC_TAIL_U];
+                // mantissas (stored for the emission / the pack) and the ten
+                // tables' total lengths, PAC_TAIL_U lines at a time (their loads
+                // in flight together)
+                const double* ln = K.lines + gl * PAC_HALFN;
+                uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
+                for (int l0 = 0; l0 < lend; l0 += PAC_TAIL_U) {
+                    double x[PAC_TAIL_U];
+                    int bal[PAC_TAIL_U], sfl[PAC_TAIL_U];
 #pragma unroll
-                for (int u = 0; u < PAC_TAIL_U; ++u) {
-                    m[u] = 0u;
-                    ent[u] = hsc;
-                    if (bal[u]) {
-                        const int ba = bal[u];
-                        m[u] = pac_mantissa(x[u], sfl[u], ba);
-                        ent[u] = hsc + (int64_t)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) * PAC_HSC_W;
+                    for (int u = 0; u < PAC_TAIL_U; ++u) {
+                        const int l = l0 + u;
+                        const int b = T->band_of_line[l];          // uniform
+                        bal[u] = l < lend ? bits_s[b][lane] : 0;
+                        sfl[u] = sf_s[b][lane];
+                        x[u] = bal[u] ? ln[l] : 0.0;
+                    }
+                    uint32_t m[PAC_TAIL_U];
+                    const uint32_t* ent[PAC_TAIL_U];
+#pragma unroll
+                    for (int u = 0; u < PAC_TAIL_U; ++u) {
+                        m[u] = 0u;
+                        ent[u] = hsc;
+                        if (bal[u]) {
+                            const int ba = bal[u];
+                            m[u] = pac_mantissa(x[u], sfl[u], ba);
+                            ent[u] = hsc + (int64_t)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) *
+                                               PAC_HSC_W;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < PAC_TAIL_U; ++u) {
+                        if (bal[u]) {
+                            const uint2 a = *reinterpret_cast<const uint2*>(ent[u]);
+                            const uint2 b2 = *reinterpret_cast<const uint2*>(ent[u] + 2);
+                            const uint32_t c4 = ent[u][4];
+                            acc[0] += a.x; acc[1] += a.y; acc[2] += b2.x; acc[3] += b2.y; acc[4] += c4;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < PAC_TAIL_U; u += 4) {      // four codes per 8-byte store
+                        const uint64_t w = (uint64_t)m[u] | ((uint64_t)m[u + 1] << 16) | ((uint64_t)m[u + 2] << 32) |
+                                           ((uint64_t)m[u + 3] << 48);
+                        *reinterpret_cast<uint64_t*>(cs + l0 + u) = w;
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < PAC_TAIL_U; ++u) {
-                    if (bal[u]) {
-                        const uint2 a = *reinterpret_cast<const uint2*>(ent[u]);
-                        const uint2 b2 = *reinterpret_cast<const uint2*>(ent[u] + 2);
-                        const uint32_t c4 = ent[u][4];
-                        acc[0] += a.x; acc[1] += a.y; acc[2] += b2.x; acc[3] += b2.y; acc[4] += c4;
-                    }
+                for (int tb = 0; tb < PAC_NTAB; ++tb) {
+                    const int v = (int)((acc[tb >> 1] >> (16 * (tb & 1))) & 0xffffu);
+                    if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
                 }
-#pragma unroll
-                for (int u = 0; u < PAC_TAIL_U; u += 4) {      // four codes per 8-byte store
-                    const uint64_t w = (uint64_t)m[u] | ((uint64_t)m[u + 1] << 16) | ((uint64_t)m[u + 2] << 32) |
-                                       ((uint64_t)m[u + 3] << 48);
-                    *reinterpret_cast<uint64_t*>(cs + l0 + u) = w;
-                }
+                dep_add += (long)orig - ((long)best + nsign + 4);
+                nb = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
+                F.tid[g] = (uint8_t)bestid;
+                F.nbytes[g] = nb;
             }
-            int best = 0, bestid = 1;
-#pragma unroll
-            for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                const int v = (int)((acc[tb >> 1] >> (16 * (tb & 1))) & 0xffffu);
-                if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
-            }
-            dep_add += (long)orig - ((long)best + nsign + 4);
-            F.tid[g] = (uint8_t)bestid;
-            F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
         }
-        deposit += dep_add;     // depositBits per channel (codec.py:120)
+        if (act) deposit += dep_add;   // depositBits per channel (codec.py:120)
     }
-    st_extra[s] = extra;
-    st_deposit[s] = deposit;
+    if (live) {
+        st_extra[s] = extra;
+        st_deposit[s] = deposit;
+    }
+}
+
+#ifndef PAC_EMIT_U
+#define PAC_EMIT_U 8      // lines per lane whose code + table loads are in flight together
+#endif
+
+// PACFile.WriteDataBlock's packing (pacfile.py:288-351) of the chunk's
+// channel-blocks, one lane per channel-block, right after the chunk's tail
+// (on its own stream, beside the next chunk's tail): '<L' nBytes, then
+// overall(4) tableID(4), per band (ba?ba-1:0)(4) sf(4) [+ the band's sign
+// bits + its Huffman codes (escape: escape code + ba raw bits)], LRMS(25)
+// [+ the short-frame bit], MSB-first, into the staging buffer -- the wave's
+// channel-blocks take consecutive pieces of one bump allocation; the offset
+// goes to F.stoff for k_master_place.  No cross-channel-block dependency, so
+// 64 per wave and many waves: the packing's latency stays off the reservoir
+// chain.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_master_emit(
+    const PacTables* __restrict__ T, const PacHuffTables* __restrict__ H, const uint64_t* __restrict__ hcode,
+    PacMasterChunkBuf K, PacMasterFields F, const int64_t* __restrict__ blk_off, PacMasterChunk ck) {
+    const int lane = threadIdx.x;
+    const int nch = ck.nch;
+    const int64_t q = (int64_t)blockIdx.x * WAVE + lane;      // chunk-local channel-block: j nch + ch
+    const int64_t j = q / nch;
+    const int ch = (int)(q % nch);
+    ChunkPos cp;
+    const bool act = j < (int64_t)ck.n_s * ck.S && chunk_block(blk_off, ck, j, &cp);
+    const int64_t gb = act ? cp.gb : 0;
+    const int64_t g = gb * nch + ch, gl = j * 2 + ch;
+    const int nb = act ? F.nbytes[g] : 0;
+    const int sz = act ? 4 + ((nb - 4 + 3) & ~3) : 0;
+    int tot;
+    const int pre = wave_excl_scan_i(sz, &tot);
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(F.stg_next, (unsigned long long)tot);
+    base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);    // 64-bit broadcast
+    const int64_t so = (int64_t)base + pre;
+    if (!act) return;
+    F.stoff[g] = so;
+    if (so + sz > F.stg_cap) return;                         // over the staging capacity: the host re-runs
+    const uint16_t* cs = K.codes + gl * PAC_HALFN;
+    const uint8_t* bag = F.ba + g * PAC_NB;
+    const uint8_t* sfg = F.sf + g * PAC_NB;
+    const int tb = F.tid[g] - 1;
+    uint32_t lrms_rev = 0;                                   // band 0 first
+    for (int b = 0; b < PAC_NB; ++b) lrms_rev = (lrms_rev << 1) | (uint32_t)(F.lrms[gb * PAC_NB + b] & 1);
+    uint32_t* w = reinterpret_cast<uint32_t*>(F.stg + so);
+    w[0] = (uint32_t)(nb - 4);
+    LaneBits out{w + 1, 0ull, 0};
+    out.put(((uint32_t)F.overall[g] << 4) | (uint32_t)(tb + 1), 8);
+    const uint32_t eb = H->esc_bits[tb];
+    const int el = H->esc_len[tb];
+    const uint64_t* hc = hcode + (int64_t)tb * PAC_NSYM;
+    for (int b = 0; b < PAC_NB; ++b) {
+        const int ba = bag[b];
+        const int nl = T->nlines[b], lo = T->lower[b];     // uniform
+        out.put(((uint32_t)(ba ? ba - 1 : 0) << 4) | sfg[b], 8);
+        if (!ba) continue;
+        uint32_t sb = 0;                                     // sign bits, 32 at a time
+        int k = 0;
+        for (int i0 = 0; i0 < nl; i0 += PAC_EMIT_U) {
+            uint32_t m[PAC_EMIT_U];
+#pragma unroll
+            for (int u = 0; u < PAC_EMIT_U; ++u) m[u] = i0 + u < nl ? cs[lo + i0 + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < PAC_EMIT_U; ++u) {
+                if (i0 + u < nl) {
+                    sb = (sb << 1) | ((m[u] >> (ba - 1)) & 1u);
+                    if (++k == 32) { out.put(sb, 32); sb = 0; k = 0; }
+                }
+            }
+        }
+        if (k) out.put(sb, k);
+        const uint32_t mask = (1u << (ba - 1)) - 1u;
+        for (int i0 = 0; i0 < nl; i0 += PAC_EMIT_U) {
+            uint32_t sym[PAC_EMIT_U];
+            uint64_t e[PAC_EMIT_U];
+#pragma unroll
+            for (int u = 0; u < PAC_EMIT_U; ++u) sym[u] = i0 + u < nl ? (cs[lo + i0 + u] & mask) : 0u;
+#pragma unroll
+            for (int u = 0; u < PAC_EMIT_U; ++u) e[u] = hc[sym[u]];
+#pragma unroll
+            for (int u = 0; u < PAC_EMIT_U; ++u) {
+                if (i0 + u < nl) {
+                    const int L = (int)(e[u] >> 32);
+                    if (L) {
+                        out.put((uint32_t)e[u], L);
+                    } else {
+                        out.put(eb, el);
+                        out.put(sym[u], ba);
+                    }
+                }
+            }
+        }
+    }
+    out.put(lrms_rev, PAC_NB);
+    if (F.bsf) out.put((uint32_t)(F.bsf[gb] & PAC_BS_SHORT ? 1 : 0), 1);
+    out.flush();
+}
+
+// Pass 2 with the tail's emission: every channel-block's bytes from the
+// staging buffer to its file offset (one wave per channel-block, 64 bytes per
+// step).  A channel-block that would end past cap is skipped; the host reports
+// PAC_E_CAPACITY from the total.
+__global__ __launch_bounds__(256) void k_master_place(PacMasterFields F, int64_t G, const int64_t* __restrict__ off,
+                                                      uint8_t* __restrict__ out, int64_t cap) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t g = (int64_t)blockIdx.x * 4 + threadIdx.x / WAVE;
+    if (g >= G) return;
+    const int nb = F.nbytes[g];
+    const int64_t og = off[g], so = F.stoff[g];
+    if (og + nb > cap || so + nb > F.stg_cap) return;
+    const uint8_t* src = F.stg + so;
+    uint8_t* dst = out + og;
+    for (int i = lane; i < nb; i += WAVE) dst[i] = src[i];
 }
 
 // worst-case master channel-block: 8 + 25 * 8 + 25 (+ 1 block-switching) bits
@@ -985,18 +1152,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 #define PACK_WORDS_MASTER ((PAC_MASTER_MAX_BITS + 31) / 32)
 static_assert(PACK_WORDS_MASTER * 4 <= 16384, "packed words must fit a 16 KB line buffer");
 
-// exclusive prefix of an int across the wave by DPP; *total = the wave's sum
-__device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
-    int x = v;
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(1), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(2), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(4), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_SHR(8), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST15, 0xa, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, PAC_DPP_BCAST31, 0xc, 0xf, false);
-    *total = __builtin_amdgcn_readlane(x, 63);
-    return x - v;
-}
 
 // Pass 2: one 256-thread workgroup per block gb (XCD-aware order):
 // PACFile.WriteDataBlock's packing of its channel-blocks (pacfile.py:288-351)

@@ -81,6 +81,50 @@ def test_chunking_invariance(ctx):
     assert chunked == full
 
 
+def _ctx_with_env(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return _lib.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("env", [{"PAC_DEBUG_STG_BIAS": 5 * 2 ** 30},   # staging offsets past 4 GiB
+                                 {"PAC_DEBUG_STG_CAP": 3000}])           # staging overflow -> the pack path
+def test_tail_emission_staging(ctx, env):
+    """The tail emits each channel-block into a staging buffer (bump-allocated
+    per wave) that k_master_place copies to the file offsets: offsets past
+    4 GiB, and a staging overflow (the call re-runs through k_master_pack
+    from the initial reservoir states), give the same bytes and states."""
+    fs = 48000
+    lens = [0, 5 * 1024 + 3, 20 * 1024, 33 * 1024 + 700]
+    streams = [synth.pink_tones_pcm(n, fs, seed=i + 11) for i, n in enumerate(lens)]
+    st0 = [_lib.StreamState() for _ in lens]
+    for i, st in enumerate(st0):
+        st.extra_bits, st.bit_deposit = 17 * i, 250 * i - 40
+    ref_states = [_lib.StreamState() for _ in lens]
+    for a, b in zip(ref_states, st0):
+        a.extra_bits, a.bit_deposit = b.extra_bits, b.bit_deposit
+    ref = pacfile.encode_streams(streams, fs, MASTER, context=ctx, states=ref_states)
+    c2 = _ctx_with_env(**env)
+    try:
+        got = pacfile.encode_streams(streams, fs, MASTER, context=c2, states=st0)
+    finally:
+        c2.close()
+    assert got == ref
+    assert [(s.extra_bits, s.bit_deposit) for s in st0] == [(s.extra_bits, s.bit_deposit) for s in ref_states]
+    o = P.Oracle(fs, huffman=True)
+    for i in (1, 3):                                   # and the oracle from the same initial states
+        st = P.State(17 * i, 250 * i - 40)
+        assert got[i] == o.encode_data(P.MASTER, streams[i], state=st)
+        assert (st.extraBits, st.deposit) == (st0[i].extra_bits, st0[i].bit_deposit)
+
+
 def test_plugin_surface_per_block_matches(ctx, tmp_path):
     """PACFile.WriteDataBlock per hop with the Huffman reservoir object, as the
     reference driver runs it (pacfile.py:474-499), equals the fixture prefix."""

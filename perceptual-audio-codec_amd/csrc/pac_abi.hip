@@ -330,6 +330,8 @@ struct pac_ctx {
     DevBuf<unsigned long long> m_stg_next;  // master: staging bump allocator
     DevBuf<uint64_t> hcode;                 // [10][PAC_NSYM] (code length << 32) | code bits, 0: escape
     DevBuf<int64_t> st_extra, st_deposit;
+    DevBuf<int32_t> m_perm;                 // master: streams by length within their group (run_master)
+    std::vector<int32_t> h_perm;            // its host copy (lives until the async upload has run)
     DevBuf<uint32_t> dbg_mant;              // per-block API: per-line mantissas and Huffman codes
     DevBuf<uint64_t> dbg_code;
     DevBuf<uint8_t> dbg_len;
@@ -414,7 +416,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
     c->m_lrms.release(); c->m_rowm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
-    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release();
+    c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->m_perm.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
     c->dec_ov.release(); c->dec_lrms.release(); c->dec_codes.release(); c->dec_so.release();
@@ -804,20 +806,34 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     const int64_t G = nch * nblocks;
     const int nvar = nch == 2 ? 6 : 1;                 // threshold variants per block
     const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : 1;
-    // chunk geometry: group [g0, g1) of at most CB streams, S blocks each
-    struct Grp { int g0, n_s, S; int64_t gmax; };
-    std::vector<Grp> groups;
+    // chunk geometry: groups [g0, g1) of at most CB streams, each ordered by
+    // length (longest first, perm); chunk = blocks t0 .. t0+S-1 of the
+    // group's streams still running at t0 (a prefix of that order), S =
+    // CB / (running streams) -- ragged stream sets keep their chunks full
+    std::vector<int32_t>& perm = c->h_perm;
+    perm.assign(n_streams, 0);
+    struct Chunk { PacMasterChunk ck; int64_t B; int n_s; };
+    std::vector<Chunk> chunks;
     int64_t cbmax = 1;
     for (int g0 = 0; g0 < n_streams;) {
         const int g1 = (int)std::min<int64_t>(n_streams, g0 + CB);
-        int64_t gmax = 1;
-        for (int k = g0; k < g1; k++) gmax = std::max<int64_t>(gmax, blk[k + 1] - blk[k]);
-        const int n_s = g1 - g0;
-        const int S = (int)std::max<int64_t>(1, std::min<int64_t>(CB / n_s, gmax));
-        groups.push_back({g0, n_s, S, gmax});
-        cbmax = std::max<int64_t>(cbmax, (int64_t)n_s * S);
+        for (int k = g0; k < g1; k++) perm[k] = k;
+        std::stable_sort(perm.begin() + g0, perm.begin() + g1,
+                         [&](int a, int b) { return blk[a + 1] - blk[a] > blk[b + 1] - blk[b]; });
+        const int64_t gmax = std::max<int64_t>(1, blk[perm[g0] + 1] - blk[perm[g0]]);
+        int n_act = g1 - g0;
+        for (int64_t t0 = 0; t0 < gmax;) {
+            while (n_act > 1 && blk[perm[g0 + n_act - 1] + 1] - blk[perm[g0 + n_act - 1]] <= t0) n_act--;
+            const int S = (int)std::max<int64_t>(1, std::min<int64_t>(CB / n_act, gmax - t0));
+            chunks.push_back({PacMasterChunk{g0, n_act, t0, S, nch, nullptr}, (int64_t)n_act * S, n_act});
+            cbmax = std::max<int64_t>(cbmax, (int64_t)n_act * S);
+            t0 += S;
+        }
         g0 = g1;
     }
+    if ((rc = c->m_perm.ensure(n_streams + 1))) return rc;
+    HIPCHK(hipMemcpyAsync(c->m_perm.p, perm.data(), n_streams * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    for (Chunk& q : chunks) q.ck.perm = c->m_perm.p;
     if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
@@ -906,11 +922,6 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipStreamWaitEvent(s2, e, 0));
         HIPCHK(hipStreamWaitEvent(s3, e, 0));
     }
-    struct Chunk { PacMasterChunk ck; int64_t B; int n_s; };
-    std::vector<Chunk> chunks;
-    for (const Grp& gr : groups)
-        for (int64_t t0 = 0; t0 < gr.gmax; t0 += gr.S)
-            chunks.push_back({PacMasterChunk{gr.g0, gr.n_s, t0, gr.S, nch}, (int64_t)gr.n_s * gr.S, gr.n_s});
     const int64_t nck = (int64_t)chunks.size();
     auto bufset = [&](int64_t i) {
         const int64_t k = i % 3;

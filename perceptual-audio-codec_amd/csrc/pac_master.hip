@@ -69,13 +69,17 @@ struct PacMasterFields {
     int64_t stg_cap;
 };
 
-// A time slice of a stream group: blocks t0 .. t0+S-1 of streams
-// s_first .. s_first+n_s-1; local block j = (s - s_first) * S + (t - t0).
+// A time slice of a stream group: blocks t0 .. t0+S-1 of the streams
+// perm[s_first .. s_first+n_s-1]; local block j = k * S + (t - t0) for the
+// stream perm[s_first + k].  run_master orders each group's streams by length
+// (longest first) and lists only the streams still running at t0, choosing
+// S per chunk, so the chunks of ragged stream sets stay full.
 struct PacMasterChunk {
     int s_first, n_s;
     int64_t t0;
     int S;
     int nch;        // 2, or 1 for the mono master extension (no LRMS, one threshold)
+    const int32_t* perm;
 };
 
 // global block id of local block j (and its stream, index in the stream),
@@ -83,7 +87,7 @@ struct PacMasterChunk {
 struct ChunkPos { int64_t gb, t; int s; };
 __device__ __forceinline__ bool chunk_block(const int64_t* __restrict__ blk_off, const PacMasterChunk& ck,
                                             int64_t j, ChunkPos* cp) {
-    const int s = ck.s_first + (int)(j / ck.S);
+    const int s = ck.perm[ck.s_first + (int)(j / ck.S)];
     const int64_t t = ck.t0 + j % ck.S;
     const int64_t b0 = blk_off[s];
     if (t >= blk_off[s + 1] - b0) return false;
@@ -929,7 +933,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int sl = blockIdx.x * WAVE + lane;
     const bool live = sl < ck.n_s;                     // every lane stays for the wave-wide steps
     const int nch = ck.nch;
-    const int s = ck.s_first + (live ? sl : 0);
+    const int s = ck.perm[ck.s_first + (live ? sl : 0)];
     const int64_t bb0 = blk_off[s];
     const int64_t len = blk_off[s + 1] - bb0;
     const int64_t t_end = !live ? ck.t0 : (ck.t0 + ck.S < len ? ck.t0 + ck.S : len);

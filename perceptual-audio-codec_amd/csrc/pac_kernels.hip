@@ -238,7 +238,7 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
                                reinterpret_cast<double2*>(xs), tid);
     PROF_MARK(4);
     const MaskerLists L = masker_lists(buf, xs);
-    int nm = grp_find_maskers<FRONT_NT>(buf, T, 15.0, tid, L);
+    int nm = grp_find_maskers<FRONT_NT>(reinterpret_cast<const double*>(buf), T, 15.0, tid, L);
     PROF_MARK(5);
     if (src.dbg & 1) nm = 0;          // diagnostic: masking sum off
     // Masking rows are claimed dynamically, most expensive first (the order
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
     const double* d = data + (int64_t)blockIdx.x * PAC_N;
     wave_spectrum_pow([&](int i) { return __dmul_rn(d[i], T->hann[i]); }, T, buf, tmp, lane);
     const MaskerLists L = masker_lists(buf, tmp);
-    const int nm = grp_find_maskers<WAVE>(buf, T, no_drop ? 0.0 : 15.0, lane, L);
+    const int nm = grp_find_maskers<WAVE>(reinterpret_cast<const double*>(buf), T, no_drop ? 0.0 : 15.0, lane, L);
 #pragma unroll 1
     for (int q = 0; q < 16; ++q)
         thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = wave_masking_row(L, nm, T, lane, q);

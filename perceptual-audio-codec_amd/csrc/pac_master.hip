@@ -133,9 +133,13 @@ __device__ __forceinline__ double2 hann_tap(double2 xm, double2 x0, double2 xp) 
     const double im = __builtin_fma(PAC_HANN_C, sy, PAC_HANN_S * dx);
     return make_double2(__builtin_fma(-0.25, re, 0.5 * x0.x), __builtin_fma(-0.25, im, 0.5 * x0.y));
 }
-// buf[k].x = |V_v[k]|^2, k < 1024; S = the block's spectra (bin k of A at
-// S[k + 2], of B at S[PAC_SPEC_LD + k + 2], k = -2..1026).  Each thread owns 4
-// consecutive bins (8 loads of the neighbourhood instead of 5 per bin).
+// ((double*)buf)[k] = |V_v[k]|^2 (dense), k < 1024; S = the block's spectra
+// (bin k of A at S[k + 2], of B at S[PAC_SPEC_LD + k + 2], k = -2..1026).
+// Each thread owns 4 consecutive bins (8 loads of the neighbourhood instead
+// of 5 per bin) and stores them as two 16-byte halves, lanes 4-7 of every 8
+// the second half first: each ds_write_b128 then covers 8 distinct 16-byte
+// bank slots (the 4 consecutive doubles at a 32-byte lane stride would be a
+// 2-way conflict, the old double2 .x layout an 8-way one).
 template <int NT>
 __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, int v, double2* buf, int tid) {
     static_assert(NT * 4 == 1024, "4 bins per thread");
@@ -159,8 +163,13 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
 #pragma unroll
         for (int i = 0; i < 4; ++i) X[i] = v < 4 ? h[i + 1] : hann_tap(h[i], h[i + 1], h[i + 2]);
     }
+    double p[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) buf[k0 + i].x = __builtin_fma(X[i].x, X[i].x, X[i].y * X[i].y);
+    for (int i = 0; i < 4; ++i) p[i] = __builtin_fma(X[i].x, X[i].x, X[i].y * X[i].y);
+    double2* pw2 = reinterpret_cast<double2*>(buf);
+    const bool sw = tid & 4;
+    pw2[2 * tid + (sw ? 1 : 0)] = sw ? make_double2(p[2], p[3]) : make_double2(p[0], p[1]);
+    pw2[2 * tid + (sw ? 0 : 1)] = sw ? make_double2(p[0], p[1]) : make_double2(p[2], p[3]);
     grp_sync<NT>();
 }
 
@@ -173,7 +182,7 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
     grp_variant_pow<FRONT_NT>(spec, v, buf, tid);
     const MaskerLists L = masker_lists(buf, tmp);
-    const int nm = grp_find_maskers<FRONT_NT>(buf, T, v >= 4 ? 0.0 : 15.0, tid, L);
+    const int nm = grp_find_maskers<FRONT_NT>(reinterpret_cast<const double*>(buf), T, v >= 4 ? 0.0 : 15.0, tid, L);
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;

@@ -499,7 +499,7 @@ __device__ __forceinline__ void grp_mdct2(const FAB& xab, const PacTables* __res
 // |FFT(d)[k]|^2, k < 1024, of a real 2048-sample block d(i) via a 1024-point
 // complex Stockham FFT.  buf and tmp: 1024 double2 of LDS each; the input
 // pairs are staged in buf, the FFT ends in tmp, and on return
-// buf[k].x = Re^2 + Im^2 (tmp is free again).  (findpeaks compares |X| and
+// ((double*)buf)[k] = Re^2 + Im^2, dense (tmp is free again).  (findpeaks compares |X| and
 // the masker SPL sums |X|^2 (psychoac.py:442-449); both only need the square.)
 // (grp_spectrum_pow_pairs: the staged pairs come from dp(n) = (d(2n), d(2n+1)).)
 template <int NT, class DP>
@@ -528,7 +528,7 @@ __device__ __forceinline__ void grp_spectrum_pow_pairs(const DP& dp, const PacTa
             double2 wo = cmul(T->rfft_tw[kk[side]], o);
             double xr = e.x + wo.y;
             double xi = e.y - wo.x;
-            buf[kk[side]].x = __builtin_fma(xr, xr, xi * xi);
+            reinterpret_cast<double*>(buf)[kk[side]] = __builtin_fma(xr, xr, xi * xi);
         }
     }
     grp_sync<NT>();
@@ -660,6 +660,15 @@ __device__ __forceinline__ MaskerLists masker_lists(void* regA, void* regB) {
     return L;
 }
 
+// Physical slot of element m of the four prefix arrays (pfh, pfl, sl, su):
+// bits 1-2 XOR bits 5-6.  The scans' lane owns 8 consecutive elements
+// (m = 8 L + k), read and written as four 16-byte pairs; the pair of lane L
+// at step c then lands in 16-byte bank slot 4 (L & 3) + (c ^ ((L >> 2) & 3)),
+// distinct across every ds_read_b128 lane group (the plain layout is a 4-way
+// conflict), while lane-consecutive accesses (the list writes) stay
+// conflict-free and a row's gathers pay one XOR per index.
+__device__ __forceinline__ int lsw(int m) { return m ^ (((m >> 5) & 3) << 1); }
+
 // DPP scans across the 64 lanes (gfx9 row_shr / row_bcast / wave_shr; lanes
 // without a source get the identity 0): inclusive prefix of a double, and of a
 // double-double (hi, lo) pair
@@ -698,10 +707,10 @@ __device__ __forceinline__ void wave_incl_scan_dd(double& h, double& l) {
 //   su:      exclusive prefix; sl: inclusive suffix (lanes own the segments in
 //            reverse order, so the lane scan runs downwards in m)
 __device__ __forceinline__ void wave_scan_flat_dd(const MaskerLists& L, int lane) {
-    const int m0 = 8 * lane;
+    const int m0 = 8 * lane, sw = ((lane >> 2) & 3) << 1;   // lsw(m0 + k) = m0 + (k ^ sw)
     double x[8], eh[8], el[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = L.pfh[m0 + k];
+    for (int k = 0; k < 8; ++k) x[k] = L.pfh[m0 + (k ^ sw)];
     double rh = 0.0, rl = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -719,33 +728,34 @@ __device__ __forceinline__ void wave_scan_flat_dd(const MaskerLists& L, int lane
     for (int k = 0; k < 8; ++k) {
         double sx, e;
         two_sum(ch, eh[k], sx, e);
-        L.pfh[m0 + k] = sx;
-        L.pfl[m0 + k] = (cl + el[k]) + e;
+        L.pfh[m0 + (k ^ sw)] = sx;
+        L.pfl[m0 + (k ^ sw)] = (cl + el[k]) + e;
     }
 }
 __device__ __forceinline__ void wave_scan_excl8(double* v, int lane) {
-    const int m0 = 8 * lane;
+    const int m0 = 8 * lane, sw = ((lane >> 2) & 3) << 1;
     double x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[m0 + k];
+    for (int k = 0; k < 8; ++k) x[k] = v[m0 + (k ^ sw)];
     double run = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { const double t = x[k]; x[k] = run; run += t; }
     const double c = dpp_f64<PAC_DPP_WSHR1>(0.0, wave_incl_scan_f64(run));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[m0 + k] = c + x[k];
+    for (int k = 0; k < 8; ++k) v[m0 + (k ^ sw)] = c + x[k];
 }
 __device__ __forceinline__ void wave_scan_suffix8(double* v, int lane) {
-    const int m0 = 8 * (WAVE - 1 - lane);
+    const int bl = WAVE - 1 - lane;
+    const int m0 = 8 * bl, sw = ((bl >> 2) & 3) << 1;
     double x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[m0 + k];
+    for (int k = 0; k < 8; ++k) x[k] = v[m0 + (k ^ sw)];
     double run = 0.0;
 #pragma unroll
     for (int k = 7; k >= 0; --k) { run += x[k]; x[k] = run; }
     const double c = dpp_f64<PAC_DPP_WSHR1>(0.0, wave_incl_scan_f64(run));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[m0 + k] = c + x[k];
+    for (int k = 0; k < 8; ++k) v[m0 + (k ^ sw)] = c + x[k];
 }
 template <int NT>
 __device__ __forceinline__ void grp_scan_lists(const MaskerLists& L, int tid) {
@@ -763,14 +773,14 @@ __device__ __forceinline__ void grp_scan_lists(const MaskerLists& L, int tid) {
     grp_sync<NT>();
 }
 
-// findpeaks (psychoac.py:158-191) on |X|^2 held in buf[k].x (the floor
+// findpeaks (psychoac.py:158-191) on |X|^2 held in pw[k] (the floor
 // 10 log10|X| > -30 is the equivalent |X|^2 > T->peak_floor2), masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
 // masker lists (MaskerLists) built by a group of NT threads.  Peaks are
 // compacted first (ballots, bin order = the reference's summation order) so
 // that the SPL (a log10 each) is evaluated once per masker.  Returns nm.
 template <int NT>
-__device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* __restrict__ T, double drop,
+__device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTables* __restrict__ T, double drop,
                                                 int tid, const MaskerLists& L) {
     constexpr int J = 1024 / NT;
     constexpr int NW = NT / WAVE;
@@ -785,8 +795,8 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
         const int k = j * NT + tid;
         bool pk = false;
         if (k >= 1 && k <= 1022) {
-            const double m = buf[k].x;
-            pk = m > buf[k - 1].x && m > buf[k + 1].x && m > floor2;
+            const double m = pw[k];
+            pk = m > pw[k - 1] && m > pw[k + 1] && m > floor2;
         }
         bal[j] = __ballot(pk);
         if (lane == 0) cnt[j * NW + w] = __popcll(bal[j]);
@@ -819,7 +829,7 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
             double s = 0.0;
             if (k >= 3) {
                 const int hi = k + 3 < 1024 ? k + 3 : 1024;
-                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, buf[i].x);   // builtin sum, from 0
+                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, pw[i]);   // builtin sum, from 0
             }
             const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
             const double sp = pac_spl(csp * s);
@@ -844,9 +854,10 @@ __device__ __forceinline__ int grp_find_maskers(double2* buf, const PacTables* _
 #pragma unroll
     for (int q = 0; q < R; ++q) {           // R * NT = 512: every slot, zero past nm
         const int idx = q * NT + tid;
-        L.pfh[idx] = rE[q];
-        L.sl[idx] = rPL[q];
-        L.su[idx] = rPU[q];
+        const int pi = lsw(idx);
+        L.pfh[pi] = rE[q];
+        L.sl[pi] = rPL[q];
+        L.su[pi] = rPU[q];
         if (idx < tot) {
             const int j = pre2[q * NW + w] + __popcll(lb[q] & below);
             L.lpre[idx] = (int16_t)j;
@@ -1045,11 +1056,12 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
     RP_T(t0);
     // flat zone [U, V): difference of the dd prefix sums (positive terms)
     double fs, fe;
-    two_sum(L.pfh[V], -L.pfh[U], fs, fe);
-    const double flat = fs + (fe + (L.pfl[V] - L.pfl[U]));
+    const int pV = lsw(V), pU = lsw(U);
+    two_sum(L.pfh[pV], -L.pfh[pU], fs, fe);
+    const double flat = fs + (fe + (L.pfl[pV] - L.pfl[pU]));
     // lower side and the quiet maskers of the upper side: factored sums
-    const double lower = L.sl[V] * T->pow_mkl[l];
-    const double upq = L.su[U] * T->pow_kl[l];
+    const double lower = L.sl[pV] * T->pow_mkl[l];
+    const double upq = L.su[pU] * T->pow_kl[l];
     const double tiq = T->tiq[l];
     RP_T(t1);
     // loud maskers below the line: loud-list ranks [0, Ul)

@@ -343,6 +343,7 @@ struct pac_ctx {
     // PAC_TAIL_MODE=serial: every master kernel on `stream` in order (nothing
     // co-runs) -- the measurement baseline of run_master's pipelined placement
     bool tail_serial = false;
+    int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -385,6 +386,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     pac_ctx* c = new pac_ctx();
     c->device = device;
     if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
+    if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -974,8 +976,14 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, spec_ready, 0));
         if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
         if ((rc = mark(1, -1))) return rc;
-        hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((q.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS, s1,
-                           T, c->hscore.p, K, F, c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
+        // few streams: a wave per stream (the one-lane chain's latency would
+        // bound the call), else a lane per stream (fewest VALU instructions)
+        if (c->tail_wide == 1 || (c->tail_wide < 0 && q.n_s <= PAC_WIDE_MAX))
+            hipLaunchKernelGGL(k_master_tail_wide, dim3((unsigned)q.n_s), dim3(WAVE), 0, s1, T, c->hscore.p, K, F,
+                               c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
+        else
+            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((q.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS,
+                               s1, T, c->hscore.p, K, F, c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
         HIPCHK(hipGetLastError());
         if ((rc = mark(1, 2))) return rc;
         tail_done[i] = event_on(s1);

@@ -1043,6 +1043,178 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     }
 }
 
+// --- the reservoir tail for few streams: one wave per stream --------------
+// The one-lane tail spends ~0.7 ms per block of a stream (its chain is a
+// string of dependent memory round trips), so a call with few streams --
+// S = 65536 / streams blocks per stream and chunk -- is bound by it.  For a
+// chunk of at most PAC_WIDE_MAX streams this kernel runs the same chain with
+// a whole wave per stream: the 25 bands in lanes 0-24 (BitAlloc's argmax as a
+// DPP + permlane reduction), 16 lines per lane for the mantissas and the
+// Huffman scoring (coalesced).  ~10x the VALU instructions per block, ~1/10
+// of the latency; the same arithmetic, so the same bytes.
+#ifndef PAC_WIDE_MAX
+#define PAC_WIDE_MAX 4096
+#endif
+
+// the first maximum of (v, b) over lanes 0-31 (larger v, then lower b),
+// wave-uniform (read from lane 0)
+template <int CTRL>
+__device__ __forceinline__ void argmax_dpp(double& v, int& b) {
+    const double ov = dpp_full_f64<CTRL>(v);
+    const int ob = __builtin_amdgcn_mov_dpp(b, CTRL, 0xf, 0xf, true);
+    const bool take = ov > v || (ov == v && ob < b);
+    v = take ? ov : v;
+    b = take ? ob : b;
+}
+__device__ __forceinline__ void argmax32(double& v, int& b) {
+    argmax_dpp<PAC_DPP_QXOR1>(v, b);
+    argmax_dpp<PAC_DPP_QXOR2>(v, b);
+    argmax_dpp<PAC_DPP_HMIRROR>(v, b);
+    argmax_dpp<PAC_DPP_MIRROR>(v, b);                  // row maxima
+    const long long iv = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)iv, (unsigned)iv, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(iv >> 32), (unsigned)(iv >> 32), false, false);
+    const auto bb = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    // lanes of row 0 get row 1's maximum in [1] (and row 1 row 0's in [0])
+    const double v0 = __longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]);
+    const double v1 = __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]);
+    const int b0 = (int)bb[0], b1 = (int)bb[1];
+    const bool take = v1 > v0 || (v1 == v0 && b1 < b0);
+    v = take ? v1 : v0;
+    b = take ? b1 : b0;
+    v = readlane_f64(v, 0);
+    b = __builtin_amdgcn_readlane(b, 0);
+}
+
+// BitAlloc of one channel-block by a wave (lane b < 25 = band b), the
+// reference's rounds as bitalloc_lane.  *ba = the lane's band allocation.
+__device__ __forceinline__ long bitalloc_wave(const int nl, const double sm, uint32_t lrms_bits, double bitBudget,
+                                              long extra, int maxMantBits, int lane, int* ba) {
+    const bool has = lane < PAC_NB;
+    int n = 0;
+    bool valid = has;
+    long total = (long)(bitBudget + (double)extra);
+    double frozen = -INFINITY;
+    while (true) {
+        double v = valid ? __builtin_fma(-6.0, (double)n, sm) : -INFINITY;
+        int b = lane;
+        argmax32(v, b);
+        if (v == -INFINITY) break;                     // no valid band left (uniform)
+        const int ib = b;
+        const int nb_ = __builtin_amdgcn_readlane(n, ib), nli = __builtin_amdgcn_readlane(nl, ib);
+        const double sv = readlane_f64(sm, ib);
+        const double gall = fmax(__builtin_fma(-6.0, (double)(nb_ - 1), sv), frozen);
+        bool drop = gall < (((lrms_bits >> ib) & 1u) ? -5.0 : -15.0);
+        int nn = nb_;
+        if (total - nli >= 0) {
+            nn = nb_ + 1;
+            total -= nli;
+            drop |= nn >= maxMantBits;
+        } else {
+            drop = true;
+        }
+        if (lane == ib) {
+            n = nn;
+            valid = !drop;
+        }
+        if (drop) frozen = fmax(frozen, __builtin_fma(-6.0, (double)(nn - 1), sv));
+    }
+    int back = 0;                                      // bits[bits == 1] = 0, their lines back
+    if (has && n == 1) { back = nl; n = 0; }
+    *ba = n;
+    return total + wave_sum_i(back) - extra;
+}
+
+__global__ __launch_bounds__(64) void k_master_tail_wide(
+    const PacTables* __restrict__ T, const uint32_t* __restrict__ hsc, PacMasterChunkBuf K, PacMasterFields F,
+    const int64_t* __restrict__ blk_off, PacMasterChunk ck, int64_t* __restrict__ st_extra,
+    int64_t* __restrict__ st_deposit, double bitBudget) {
+    __shared__ uint8_t ba_s[32], sf_s[32];
+    const int lane = threadIdx.x;
+    const int sl = blockIdx.x;
+    const int nch = ck.nch;
+    const int s = ck.perm[ck.s_first + sl];
+    const int64_t bb0 = blk_off[s];
+    const int64_t len = blk_off[s + 1] - bb0;
+    const int64_t t_end = ck.t0 + ck.S < len ? ck.t0 + ck.S : len;
+    long extra = st_extra[s], deposit = st_deposit[s];
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    const bool has = lane < PAC_NB;
+    const int nl = has ? T->nlines[lane] : 0;
+    for (int64_t t = ck.t0; t < t_end; ++t) {
+        const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
+        const int64_t gb = bb0 + t;
+        // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
+        long e = 0;
+        if (deposit > 10) { e = deposit / 100; deposit -= e; }
+        else if (deposit < 0) { e = deposit; deposit = 0; }
+        extra += e;
+        const uint32_t lrms_bits =
+            (uint32_t)__ballot(has && F.lrms[gb * PAC_NB + (has ? lane : 0)] != 0) & ((1u << PAC_NB) - 1u);
+        long dep_add = 0;
+        for (int ch = 0; ch < nch; ++ch) {
+            const int64_t gl = j * 2 + ch, g = gb * nch + ch;
+            uint16_t* cs = F.codes ? F.codes + g * PAC_HALFN : K.codes + gl * PAC_HALFN;
+            const double sm = has ? K.smr[gl * PAC_NB + lane] : 0.0;
+            int ba;
+            extra += bitalloc_wave(nl, sm, lrms_bits, bitBudget, extra, 16, lane, &ba);
+            int f = 0;
+            if (has) {
+                f = pac_scale_factor(K.bandpeak[gl * PAC_NB + lane], ba);
+                ba_s[lane] = (uint8_t)ba;
+                sf_s[lane] = (uint8_t)f;
+                F.ba[g * PAC_NB + lane] = (uint8_t)ba;
+                F.sf[g * PAC_NB + lane] = (uint8_t)f;
+            }
+            const int orig = wave_sum_i(has ? ba * nl : 0);
+            const int nsign = wave_sum_i(has && ba ? nl : 0);
+            wave_sync();                               // ba_s / sf_s visible
+            const double* ln = K.lines + gl * PAC_HALFN;
+            uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll 4
+            for (int q = 0; q < PAC_HALFN / WAVE; ++q) {
+                const int l = q * WAVE + lane;
+                uint32_t m = 0u;
+                if (l < lend) {
+                    const int b = T->band_of_line[l];
+                    const int bl = ba_s[b];
+                    if (bl) {
+                        m = pac_mantissa(ln[l], sf_s[b], bl);
+                        const uint32_t* en = hsc + (int64_t)(((1 << (bl - 1)) - 2) + (m & ((1u << (bl - 1)) - 1u))) *
+                                                       PAC_HSC_W;
+                        const uint2 a = *reinterpret_cast<const uint2*>(en);
+                        const uint2 b2 = *reinterpret_cast<const uint2*>(en + 2);
+                        acc[0] += a.x; acc[1] += a.y; acc[2] += b2.x; acc[3] += b2.y; acc[4] += en[4];
+                    }
+                }
+                cs[l] = (uint16_t)m;
+            }
+            int best = 0, bestid = 1;
+#pragma unroll
+            for (int w = 0; w < 5; ++w) {
+                const uint32_t tot = (uint32_t)wave_sum_i((int)acc[w]);   // two 16-bit fields, no carry across
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int tb = 2 * w + h;
+                    const int v = (int)((tot >> (16 * h)) & 0xffffu);
+                    if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
+                }
+            }
+            dep_add += (long)orig - ((long)best + nsign + 4);
+            if (lane == 0) {
+                F.tid[g] = (uint8_t)bestid;
+                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
+            }
+            wave_sync();                               // ba_s / sf_s rewritten by the next channel
+        }
+        deposit += dep_add;   // depositBits per channel (codec.py:120)
+    }
+    if (lane == 0) {
+        st_extra[s] = extra;
+        st_deposit[s] = deposit;
+    }
+}
+
 #ifndef PAC_EMIT_U
 #define PAC_EMIT_U 8      // lines per lane whose code + table loads are in flight together
 #endif

@@ -125,6 +125,30 @@ def test_tail_emission_staging(ctx, env):
         assert (st.extraBits, st.deposit) == (st0[i].extra_bits, st0[i].bit_deposit)
 
 
+@pytest.mark.parametrize("wide", [0, 1])
+def test_tail_variants_vs_oracle(ctx, wide):
+    """Both reservoir tails -- one lane per stream (many streams) and one wave
+    per stream (few streams, the default below PAC_WIDE_MAX) -- give the
+    oracle's bytes and reservoir states on ragged streams."""
+    fs = 44100
+    lens = [0, 700, 1024, 9 * 1024 + 77, 22 * 1024, 31 * 1024 + 5]
+    streams = [synth.pink_tones_pcm(n, fs, seed=40 + i) if i % 2 else synth.white_pcm(n, 2, seed=50 + i)
+               for i, n in enumerate(lens)]
+    states = [_lib.StreamState() for _ in lens]
+    for i, st in enumerate(states):
+        st.extra_bits, st.bit_deposit = 5 * i, 300 * i - 7
+    c2 = _ctx_with_env(PAC_TAIL_WIDE=wide)
+    try:
+        got = pacfile.encode_streams(streams, fs, MASTER, context=c2, states=states)
+    finally:
+        c2.close()
+    o = P.Oracle(fs, huffman=True)
+    for i, pcm in enumerate(streams):
+        st = P.State(5 * i, 300 * i - 7)
+        assert got[i] == o.encode_data(P.MASTER, pcm, state=st), "stream %d" % i
+        assert (states[i].extra_bits, states[i].bit_deposit) == (st.extraBits, st.deposit)
+
+
 def test_plugin_surface_per_block_matches(ctx, tmp_path):
     """PACFile.WriteDataBlock per hop with the Huffman reservoir object, as the
     reference driver runs it (pacfile.py:474-499), equals the fixture prefix."""

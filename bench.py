@@ -566,6 +566,10 @@ def main():
     value = total_blocks / (el_max / a.steps)
 
     kern_ms = {k: float(np.mean([p[f] for p in per])) for f, k in PHASES["bs" if a.bs else a.profile]}
+    if a.master and kern_ms.get("k_master_lrms") == 0.0 and "k_master_spec" in kern_ms:
+        # the default fused LRMS + spectra kernel is timed in the spectra phase
+        del kern_ms["k_master_lrms"]
+        kern_ms["k_master_lrms_spec"] = kern_ms.pop("k_master_spec")
     # the dominant kernel on the critical path (the master reservoir tail runs on
     # a second stream, overlapped with the next chunk's thresholds)
     dom = max((k for k in kern_ms if k not in ("k_master_tail", "k_master_emit")), key=kern_ms.get)

@@ -102,7 +102,8 @@ typedef struct {
     float thr_ms;
     float lrms_ms;
     float thr_short_ms; /* block switching: k_master_thr_short (the short frames' thresholds) */
-    float spec_ms;      /* master: k_master_spec (the windowed L/R spectra the thresholds derive from) */
+    float spec_ms;      /* master: k_master_spec (the windowed L/R spectra the thresholds derive from), or the
+                           default fused k_master_lrms_spec (LRMS + spectra; lrms_ms is then 0) */
     float emit_ms;      /* master: k_master_emit (the bitstream packing beside the next chunk's tail; pack_ms
                            is then k_master_place, the copy to the file offsets) */
 } pac_timing;

@@ -344,6 +344,7 @@ struct pac_ctx {
     // co-runs) -- the measurement baseline of run_master's pipelined placement
     bool tail_serial = false;
     int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
+    bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -387,6 +388,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     c->device = device;
     if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
     if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
+    if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -936,6 +938,11 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         const Chunk& q = chunks[i];
         const PacMasterChunkBuf K = bufset(i);
         if ((rc2 = mark(2, -1))) return rc2;
+        if (c->side_fused) {          // timed as the spectra phase (spec_ms), lrms_ms = 0
+            hipLaunchKernelGGL(k_master_lrms_spec, dim3((unsigned)q.B), dim3(256), 0, s2, src, T, K, F, q.ck);
+            HIPCHK(hipGetLastError());
+            return mark(2, 7);
+        }
         if (nch == 2) hipLaunchKernelGGL(k_master_lrms, dim3((unsigned)q.B), dim3(256), 0, s2, src, T, F, q.ck);
         if ((rc2 = mark(2, 5))) return rc2;
         hipLaunchKernelGGL(k_master_spec, dim3((unsigned)q.B), dim3(256), 0, s2, src, T, K, F, q.ck);

@@ -470,13 +470,10 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
 // |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band, over the complex FFT bins
 // of the raw (unwindowed) blocks, with numpy's pairwise sums.  It runs first so
 // that k_master_thr computes only the thresholds a band's coding mode uses.
-__global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTables* __restrict__ T,
-                                                     PacMasterFields F, PacMasterChunk ck) {
-    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
+__device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables* __restrict__ T,
+                                           const PacMasterFields& F, const ChunkPos& cp, double2* bufA,
+                                           double2* bufB) {
     const int tid = threadIdx.x;
-    const int64_t j = blockIdx.x;
-    ChunkPos cp;
-    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
     const int64_t gb = cp.gb;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
@@ -571,19 +568,26 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     }
 }
 
+
+__global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTables* __restrict__ T,
+                                                     PacMasterFields F, PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
+    lrms_block(src, T, F, cp, bufA, bufB);
+}
+
 // One 256-thread workgroup per stereo block: the complex spectra A = FFT(a),
 // B = FFT(b), bins 0..1024, of the two channels' windowed blocks
 // a = (x_L w) hann, b = (x_R w) hann (the first in-place chains of
 // EncodeDualChannel / calcBTHR, psychoac.py:540-545) -> K.spec, from which
 // k_master_thr derives all six threshold variants' spectra (grp_variant_pow).
-__global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTables* __restrict__ T,
-                                                     PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
-    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
+__device__ __forceinline__ void spec_block(const PacSource& src, const PacTables* __restrict__ T,
+                                           const PacMasterChunkBuf& K, const PacMasterFields& F,
+                                           const PacMasterChunk& ck, const ChunkPos& cp, int64_t j, double2* bufA,
+                                           double2* bufB) {
     double nyq[2] = {0.0, 0.0};   // thread 0's registers (the split's pair p = 0): 32 KB LDS, 5 WG/CU
     const int tid = threadIdx.x;
-    const int64_t j = blockIdx.x;
-    ChunkPos cp;
-    if (!chunk_block(src.blk_off, ck, j, &cp)) return;
     const int64_t gb = cp.gb;
     const int fl = F.bsf ? F.bsf[gb] : 0;
     if (fl & PAC_BS_SHORT) return;                 // k_master_thr_short's
@@ -625,6 +629,28 @@ __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTab
             q[1026] = make_double2(X[1022].x, -X[1022].y);
         }
     }
+}
+
+
+__global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTables* __restrict__ T,
+                                                     PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
+    spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
+}
+
+// Both, one workgroup per block: the LRMS decisions, then the windowed
+// spectra in the same 32 KB (one launch and one workgroup prologue per block
+// on the side stream instead of two).
+__global__ __launch_bounds__(256) void k_master_lrms_spec(PacSource src, const PacTables* __restrict__ T,
+                                                          PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
+    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
+    ChunkPos cp;
+    if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
+    if (ck.nch == 2) lrms_block(src, T, F, cp, bufA, bufB);
+    __syncthreads();                              // the leaf sums are read before the spectra overwrite them
+    spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
 }
 
 // lane i <- lane i + OFF of its DPP row (row_shl:OFF; bound_ctrl: 0 past the

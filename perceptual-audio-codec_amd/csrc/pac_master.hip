@@ -31,6 +31,15 @@
 
 #include "pac_bs.h"
 
+// diagnostic (PAC_DEBUG_FLAGS 32 / 64, run_master): shader clock at phase mark
+// k of every wave of the first PAC_PROF_WG workgroups of a launch
+#define MPROF(k)                                                                                     \
+    do {                                                                                             \
+        if (src.prof && blockIdx.x < PAC_PROF_WG && (threadIdx.x & (WAVE - 1)) == 0)                 \
+            src.prof[((int64_t)blockIdx.x * 4 + threadIdx.x / WAVE) * PAC_PROF_MARKS + (k)] =        \
+                (long long)__builtin_amdgcn_s_memtime();                                             \
+    } while (0)
+
 // chunk-local scratch, local block j (thr and spec single-buffered, ordered by
 // events in run_master; lines / smr / bandpeak triple-buffered between the
 // front of chunk i and its tail, which runs beside chunk i+1's thresholds)
@@ -186,7 +195,7 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
-    __syncthreads();
+    lds_sync();
 #pragma unroll 1
     while (true) {
         int k = 0;
@@ -236,7 +245,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
     thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid);
     if (ck.nch != 2) return;
-    __syncthreads();                                        // the first variant's lists are read
+    lds_sync();                                             // the first variant's lists are read
     int t2 = tid;                // opaque copy: no per-lane address of the first call is kept live for the second
     asm volatile("" : "+v"(t2));
     thr_variant(T, spec, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2);
@@ -493,6 +502,7 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         nlb = T->nlines[tid];
         lob = T->lower[tid];
     }
+    MPROF(0);
     if (!rL.f) {
         grp_spectrum_cplx2p<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
             const double2 f0 = stereo_frame(rL, 2 * n), f1 = stereo_frame(rL, 2 * n + 1);
@@ -503,6 +513,7 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             return make_double4(rL(2 * n), rL(2 * n + 1), rR(2 * n), rR(2 * n + 1));
         }, T, bufA, bufB, tid);
     }
+    MPROF(1);
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
@@ -544,11 +555,11 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             lv1.x = __dadd_rn(lv1.x, sm.x); lv1.y = __dadd_rn(lv1.y, sm.y);
         }
     }
-    __syncthreads();                               // every spectrum read: bufA's start holds the leaves
+    lds_sync();                                    // every spectrum read: bufA's start holds the leaves
     double2* leafv0 = bufA;
     double2* leafv1 = bufA + 64;
     if (has && sub == 0) { leafv0[lf] = lv0; leafv1[lf] = lv1; }
-    __syncthreads();
+    lds_sync();
     if (tid < WAVE) {                              // wave 0: the decisions and the rows they select
         int rows = 0;
         if (tid < PAC_NB) {
@@ -566,6 +577,7 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         rows = wave_or_i(rows);
         if (tid == 0) F.rowm[gb] = (uint32_t)rows;
     }
+    MPROF(2);
 }
 
 
@@ -609,6 +621,7 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
                                 variant_sample(rL, rR, T, 1, 2 * n, fl), variant_sample(rL, rR, T, 1, 2 * n + 1, fl));
         }, T, bufA, bufB, tid, nyq);
     }
+    MPROF(3);
     // bins -2..1026 at o[bin + 2]: the mirrored edge bins X[-k] = X[2048-k] =
     // conj X[k] stored, so the taps of k_master_thr need no index arithmetic
     double2* o = K.spec + j * 2 * PAC_SPEC_LD + 2;
@@ -629,6 +642,7 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
             q[1026] = make_double2(X[1022].x, -X[1022].y);
         }
     }
+    MPROF(4);
 }
 
 
@@ -649,7 +663,7 @@ __global__ __launch_bounds__(256) void k_master_lrms_spec(PacSource src, const P
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
     if (ck.nch == 2) lrms_block(src, T, F, cp, bufA, bufB);
-    __syncthreads();                              // the leaf sums are read before the spectra overwrite them
+    lds_sync();                                   // the leaf sums are read before the spectra overwrite them
     spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
 }
 
@@ -678,14 +692,13 @@ __device__ __forceinline__ void seg_max_step(unsigned long long& k0, unsigned lo
 // lines, MLD threshold combination, SMR selection and the band maxima (LDS
 // atomic max on order-preserving keys).  Only the thresholds of each band's
 // coding mode are read (k_master_thr computes no others).
-__global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTables* __restrict__ T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_master_front(PacSource src, const PacTables* __restrict__ T,
                                                       PacMasterChunkBuf K, PacMasterFields F,
                                                       PacMasterChunk ck) {
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB (5 workgroups per CU)
     // after the MDCTs: SMR 0/1, |line| 0/1, max|X| L/R keys and the LRMS flags
     // in the free upper half of bufB
     unsigned long long (*key)[32] = reinterpret_cast<unsigned long long (*)[32]>(bufB + 512);
-    uint8_t* lrms_s = reinterpret_cast<uint8_t*>(bufB + 640);
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     ChunkPos cp;
@@ -696,6 +709,17 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
     const bool sh = fl & PAC_BS_SHORT;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
+    // each thread's four lines l = 256 i + tid: band and coding mode, loaded
+    // before the MDCT so that the threshold loads can all issue right after it
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    int bl4[4], ms4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int l = i * 256 + tid;
+        bl4[i] = T->band_of_line[l];
+        ms4[i] = l < lend ? F.lrms[gb * PAC_NB + bl4[i]] : 0;
+    }
+    MPROF(0);
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
     const double* XL;
@@ -729,9 +753,27 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
     }
     // (every MDCT ended with a barrier: the upper halves are free)
+    MPROF(1);
+    // the thresholds of the four lines' coding modes, all loads in flight
+    // together (the selection loop below stores to HBM, which the compiler
+    // cannot move these loads across): L, R or M, S and the MLD-scaled M, S
+    const double* thr = K.thr + j * 6 * PAC_HALFN;
+    double t4[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int l = i * 256 + tid;
+        const double* tp = thr + (ms4[i] ? 2 * PAC_HALFN : 0) + l;
+        t4[i][0] = tp[0];
+        t4[i][1] = tp[PAC_HALFN];
+        t4[i][2] = t4[i][3] = 0.0;
+        if (ms4[i]) {
+            const double mld = sh ? T->mld_s[l >> 2] : T->mld[l];
+            t4[i][2] = __dmul_rn(tp[2 * PAC_HALFN], mld);
+            t4[i][3] = __dmul_rn(tp[3 * PAC_HALFN], mld);
+        }
+    }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
-    if (tid < PAC_NB) lrms_s[tid] = F.lrms[gb * PAC_NB + tid];
-    __syncthreads();
+    lds_sync();
     double xl4[4], xr4[4];
     double mL = 0.0, mR = 0.0;
 #pragma unroll
@@ -747,33 +789,30 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
         atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
         atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
     }
-    __syncthreads();
+    lds_sync();
     const int oL = pac_scale_factor(__longlong_as_double((long long)key[4][0]), 5);
     const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
     const double gL = (double)(1 << oL), gR = (double)(1 << oR);
     const double offL = 6.02 * oL, offR = 6.02 * oR;
+    MPROF(2);
     if (tid == 0) {
         F.overall[gb * ck.nch] = (uint8_t)oL;
         if (st) F.overall[gb * 2 + 1] = (uint8_t)oR;
     }
 
     // --- per-line SMR terms (psychoac.py:533-597), selection (:662-682) ----
-    const double* thr = K.thr + j * 6 * PAC_HALFN;
     double* lines = K.lines + j * 2 * PAC_HALFN;
-    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = i * 256 + tid;
         const double xl = __dmul_rn(xl4[i], gL), xr = __dmul_rn(xr4[i], gR);
         const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
-        const int b = T->band_of_line[l];
-        const int ms = l < lend ? lrms_s[b] : 0;
+        const int b = bl4[i];
+        const int ms = ms4[i];
         double d0, d1;
         if (ms) {
-            const double bM = thr[2 * PAC_HALFN + l], bS = thr[3 * PAC_HALFN + l];
-            const double bMm = thr[4 * PAC_HALFN + l], bSm = thr[5 * PAC_HALFN + l];
-            const double mld = sh ? T->mld_s[l >> 2] : T->mld[l];
-            const double mldM = __dmul_rn(bMm, mld), mldS = __dmul_rn(bSm, mld);
+            const double bM = t4[i][0], bS = t4[i][1];
+            const double mldM = t4[i][2], mldS = t4[i][3];
             const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
             const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
             const double c = bM < mldM ? bM : mldM;
@@ -781,8 +820,8 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
             d0 = (pac_spl(4. * (M * M)) - offL) - thrM;
             d1 = (pac_spl(4. * (S * S)) - offR) - thrS;
         } else {
-            d0 = (pac_spl(4. * (xl * xl)) - offL) - thr[0 * PAC_HALFN + l];
-            d1 = st ? (pac_spl(4. * (xr * xr)) - offR) - thr[1 * PAC_HALFN + l] : 0.0;
+            d0 = (pac_spl(4. * (xl * xl)) - offL) - t4[i][0];
+            d1 = st ? (pac_spl(4. * (xr * xr)) - offR) - t4[i][1] : 0.0;
         }
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;
@@ -808,7 +847,8 @@ __global__ __launch_bounds__(256) void k_master_front(PacSource src, const PacTa
             atomicMax(&key[3][b], k3);
         }
     }
-    __syncthreads();
+    lds_sync();
+    MPROF(3);
     if (tid < PAC_NB) {
         const bool has = T->nlines[tid] != 0;
         K.smr[(j * 2 + 0) * PAC_NB + tid] = has ? pac_order_unkey(key[0][tid]) : -96.0;

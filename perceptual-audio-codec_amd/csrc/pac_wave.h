@@ -12,12 +12,26 @@
 
 #define WAVE 64
 
+// The barriers of these kernels hand off LDS only (no workgroup passes data
+// to itself through global memory), so their fences are restricted to the
+// local address space: they drain LDS operations (lgkmcnt) but leave global
+// loads in flight -- a plain workgroup fence also waits for every outstanding
+// global load (vmcnt), which serialised table and threshold loads with the
+// barriers of each FFT stage.
+
 __device__ __forceinline__ void wave_sync() {
     // LDS hand-off between lanes of one wave: drain this wave's LDS ops and
-    // keep the compiler from moving accesses across (waves never share LDS).
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // keep the compiler from moving LDS accesses across (waves never share LDS).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// workgroup barrier for an LDS hand-off
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 
@@ -87,7 +101,7 @@ __device__ __forceinline__ unsigned brev(unsigned x, int bits) {
 
 template <int NT>
 __device__ __forceinline__ void grp_sync() {
-    if constexpr (NT == WAVE) wave_sync(); else __syncthreads();
+    if constexpr (NT == WAVE) wave_sync(); else lds_sync();
 }
 
 // In-place radix-2 DIT FFT of n = 2^LOG complex values that were stored in

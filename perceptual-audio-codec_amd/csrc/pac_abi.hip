@@ -340,13 +340,11 @@ struct pac_ctx {
     hipStream_t stream2 = nullptr;          // master: the reservoir tail, overlapping the next chunk
     hipStream_t stream3 = nullptr;          // master: the next chunk's LRMS decisions and spectra
     hipStream_t stream4 = nullptr;          // master: the bitstream emission of the previous chunk
-    hipStream_t stream5 = nullptr;          // master (PAC_FRONT_ASYNC=1): the front, beside the next thresholds
     // PAC_TAIL_MODE=serial: every master kernel on `stream` in order (nothing
     // co-runs) -- the measurement baseline of run_master's pipelined placement
     bool tail_serial = false;
     int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
     bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
-    bool front_async = false;              // PAC_FRONT_ASYNC=1: thresholds double-buffered, front(i) beside thr(i+1)
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -391,14 +389,12 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
     if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
-    if (const char* f = getenv("PAC_FRONT_ASYNC")) c->front_async = atoi(f) != 0;
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
                     hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
                     hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) == hipSuccess;
+                    hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
@@ -417,7 +413,6 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamSynchronize(c->stream2);
     hipStreamSynchronize(c->stream3);
     hipStreamSynchronize(c->stream4);
-    hipStreamSynchronize(c->stream5);
     for (auto& kv : c->tables) hipFree(kv.second);
     c->hscore.release(); c->hcode.release(); c->m_ccodes.release(); c->m_stg.release(); c->m_stoff.release();
     c->m_stg_next.release();
@@ -444,7 +439,6 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     hipStreamDestroy(c->stream2);
     hipStreamDestroy(c->stream3);
     hipStreamDestroy(c->stream4);
-    hipStreamDestroy(c->stream5);
     delete c;
 }
 
@@ -848,7 +842,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure((c->front_async ? 2 : 1) * cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(3 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(3 * cbmax * 2 * PAC_NB)))
         return rc;
     pack = pack || dbg_codes;
@@ -906,19 +900,17 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     const bool serial = c->tail_serial;
     hipStream_t s0 = c->stream, s1 = serial ? c->stream : c->stream2, s2 = serial ? c->stream : c->stream3;
     hipStream_t s3 = serial ? c->stream : c->stream4;
-    const bool fasync = c->front_async && !serial;
-    hipStream_t s4 = fasync ? c->stream5 : s0;     // the front
     const double budget = bit_budget(p);
     // timing: events recorded around every launch on its own stream, read
     // once after the call; mk[k] = (pool event, phase) of stream k, phase -1
     // opens an interval, phase >= 0 closes one
-    std::vector<std::pair<size_t, int>> mk[5];
+    std::vector<std::pair<size_t, int>> mk[4];
     size_t nev = 0;
     auto mark = [&](int k, int phase) -> int {
         if (!c->timing) return PAC_OK;
         const hipEvent_t e = c->pool_event(nev);
         mk[k].emplace_back(nev++, phase);
-        HIPCHK(hipEventRecord(e, k == 4 ? s4 : k == 3 ? s3 : k == 2 ? s2 : (k ? s1 : s0)));
+        HIPCHK(hipEventRecord(e, k == 3 ? s3 : k == 2 ? s2 : (k ? s1 : s0)));
         return PAC_OK;
     };
     auto event_on = [&](hipStream_t st) -> hipEvent_t {   // a fresh ordering event (no timing)
@@ -933,12 +925,11 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipStreamWaitEvent(s1, e, 0));
         HIPCHK(hipStreamWaitEvent(s2, e, 0));
         HIPCHK(hipStreamWaitEvent(s3, e, 0));
-        if (fasync) HIPCHK(hipStreamWaitEvent(s4, e, 0));
     }
     const int64_t nck = (int64_t)chunks.size();
     auto bufset = [&](int64_t i) {
         const int64_t k = i % 3;
-        return PacMasterChunkBuf{c->m_thr.p + (fasync ? (i & 1) * cbmax * 6 * PAC_HALFN : 0), c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
+        return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
                                  c->m_spec.p, c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN};
     };
@@ -969,15 +960,14 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         if ((rc2 = mark(2, 7))) return rc2;
         return PAC_OK;
     };
-    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr), front_done(nck, nullptr);
+    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr);
     if ((rc = launch_side(0))) return rc;
     hipEvent_t spec_ready = event_on(s2);
     for (int64_t i = 0; i < nck; ++i) {
         const Chunk& q = chunks[i];
         const PacMasterChunkBuf K = bufset(i);
         HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
-        if (i >= 3 && !fasync) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
-        if (fasync && i >= 2) HIPCHK(hipStreamWaitEvent(s0, front_done[i - 2], 0));  // thresholds set i & 1 read
+        if (i >= 3) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
         if ((rc = mark(0, -1))) return rc;
         hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
                            T, K, F, q.ck);
@@ -993,19 +983,13 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             if ((rc = launch_side(i + 1))) return rc;
             spec_ready = event_on(s2);
         }
-        if (fasync) {                                 // the front on its own stream, beside thr(i + 1)
-            HIPCHK(hipStreamWaitEvent(s4, thr_done, 0));
-            if (i >= 3) HIPCHK(hipStreamWaitEvent(s4, tail_done[i - 3], 0));   // set k's last reader
-        }
-        const int kf = fasync ? 4 : 0;
-        if ((rc = mark(kf, -1))) return rc;
-        hipLaunchKernelGGL(k_master_front, dim3((unsigned)q.B), dim3(256), 0, s4, src_front, T, K, F, q.ck);
+        if ((rc = mark(0, -1))) return rc;
+        hipLaunchKernelGGL(k_master_front, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
         HIPCHK(hipGetLastError());
-        if ((rc = mark(kf, 1))) return rc;
-        front_done[i] = event_on(s4);
+        if ((rc = mark(0, 1))) return rc;
         // the tail of this chunk once the next chunk's spectra are ready too,
         // i.e. beside the next chunk's thresholds
-        HIPCHK(hipStreamWaitEvent(s1, front_done[i], 0));
+        HIPCHK(hipStreamWaitEvent(s1, event_on(s0), 0));
         if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, spec_ready, 0));
         if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
         if ((rc = mark(1, -1))) return rc;
@@ -1032,7 +1016,6 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     }
     HIPCHK(hipStreamWaitEvent(s0, event_on(s1), 0));
     HIPCHK(hipStreamWaitEvent(s0, event_on(s3), 0));
-    if (fasync) HIPCHK(hipStreamWaitEvent(s0, event_on(s4), 0));
     if (c->dbg & (32 | 64)) {
         HIPCHK(hipStreamWaitEvent(s0, event_on(s2), 0));
         if ((rc = report_phase_clocks(c, s0, nprof))) return rc;
@@ -1060,7 +1043,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     if (c->timing) {
         HIPCHK(hipStreamSynchronize(s0));
         float ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = 0; k < 5; k++)
+        for (int k = 0; k < 4; k++)
             for (size_t j = 1; j < mk[k].size(); j++) {
                 if (mk[k][j].second < 0) continue;
                 float ms = 0.f;

@@ -323,6 +323,7 @@ struct pac_ctx {
     DevBuf<double2> m_spec;               // [chunk][2][PAC_SPEC_LD] k_master_spec -> k_master_thr
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
     DevBuf<uint32_t> m_rowm;                // [nblocks] k_master_lrms -> k_master_thr row masks
+    DevBuf<uint32_t> m_msm;                 // [nblocks] k_master_lrms -> k_master_front LRMS band masks
     DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack; pack path only)
     DevBuf<uint16_t> m_ccodes;              // master: the chunk's codes, tail-internal (emission path)
     DevBuf<uint8_t> m_stg;                  // master: channel-blocks emitted by the tail (staging)
@@ -419,7 +420,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
-    c->m_lrms.release(); c->m_rowm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
+    c->m_lrms.release(); c->m_rowm.release(); c->m_msm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->m_perm.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
@@ -838,7 +839,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     if ((rc = c->m_perm.ensure(n_streams + 1))) return rc;
     HIPCHK(hipMemcpyAsync(c->m_perm.p, perm.data(), n_streams * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     for (Chunk& q : chunks) q.ck.perm = c->m_perm.p;
-    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
+    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_msm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
@@ -847,7 +848,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         return rc;
     pack = pack || dbg_codes;
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
-                      nullptr, nullptr, nullptr, nullptr, nullptr, c->m_rowm.p, nullptr, nullptr, nullptr, 0};
+                      nullptr, nullptr, nullptr, nullptr, nullptr, c->m_rowm.p, nullptr, nullptr, nullptr, 0,
+                      c->m_msm.p};
     if (pack) {
         if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
         F.codes = c->m_codes.p;

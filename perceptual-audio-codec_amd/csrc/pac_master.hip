@@ -76,6 +76,7 @@ struct PacMasterFields {
     int64_t* stoff;      // [G]
     unsigned long long* stg_next;   // bump allocator of stg
     int64_t stg_cap;
+    uint32_t* msm;       // [nblocks] the LRMS flags as a band mask (bit b: band b M/S), k_master_lrms
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of the streams
@@ -204,7 +205,10 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
         if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
-        out[r * WAVE + lane] = wave_masking_row(L, nm, T, lane, r);
+        const double t = wave_masking_row(L, nm, T, lane, r);
+        // the MLD pair is stored as MLD_M / MLD_S = BTHR_*_MLD * mld (psychoac.py:582-583),
+        // the only form k_master_front reads
+        out[r * WAVE + lane] = v >= 4 ? __dmul_rn(t, T->mld[r * WAVE + lane]) : t;
     }
 }
 
@@ -303,7 +307,7 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw, lane);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     wave_threshold_short(reinterpret_cast<char*>(bufs[k][0]), T, v >= 4 ? 0.0 : 15.0, lane, rows,
-                         [&](int l, double t) { out[4 * l + k] = t; });
+                         [&](int l, double t) { out[4 * l + k] = v >= 4 ? __dmul_rn(t, T->mld_s[l]) : t; });
 }
 
 // Block switching: attack flags, one wave per two blocks.  Lane (b, c, s)
@@ -561,13 +565,13 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
     if (has && sub == 0) { leafv0[lf] = lv0; leafv1[lf] = lv1; }
     lds_sync();
     if (tid < WAVE) {                              // wave 0: the decisions and the rows they select
-        int rows = 0;
+        int rows = 0, ms = 0;
         if (tid < PAC_NB) {
             int i0 = fl0, i1 = i0;
             const int nl = nlb;
             const double2 sd = np_csum_combine<5>(leafv0, i0, 2 * nl);
             const double2 ss = np_csum_combine<5>(leafv1, i1, 2 * nl);
-            const int ms = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
+            ms = hypot(sd.x, sd.y) < 0.8 * hypot(ss.x, ss.y) ? 1 : 0;
             F.lrms[gb * PAC_NB + tid] = (uint8_t)ms;
             if (nl) {                              // the 64-line rows of the band's lines
                 const int r0 = lob / WAVE, r1 = (lob + nl - 1) / WAVE;
@@ -575,7 +579,11 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             }
         }
         rows = wave_or_i(rows);
-        if (tid == 0) F.rowm[gb] = (uint32_t)rows;
+        const uint32_t msm = (uint32_t)__ballot(ms);
+        if (tid == 0) {
+            F.rowm[gb] = (uint32_t)rows;
+            F.msm[gb] = msm;
+        }
     }
     MPROF(2);
 }
@@ -709,16 +717,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const bool sh = fl & PAC_BS_SHORT;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
-    // each thread's four lines l = 256 i + tid: band and coding mode, loaded
-    // before the MDCT so that the threshold loads can all issue right after it
+    // each thread's four lines l = 256 i + tid: bands, and the block's LRMS
+    // band mask, loaded before the MDCT (no wait: the LDS barriers leave them
+    // in flight) so that the threshold loads can all issue right after it
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-    int bl4[4], ms4[4];
+    int bl4[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int l = i * 256 + tid;
-        bl4[i] = T->band_of_line[l];
-        ms4[i] = l < lend ? F.lrms[gb * PAC_NB + bl4[i]] : 0;
-    }
+    for (int i = 0; i < 4; ++i) bl4[i] = T->band_of_line[i * 256 + tid];
+    const uint32_t msm = st ? F.msm[gb] : 0u;     // mono: all L/R
     MPROF(0);
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
@@ -758,19 +764,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // together (the selection loop below stores to HBM, which the compiler
     // cannot move these loads across): L, R or M, S and the MLD-scaled M, S
     const double* thr = K.thr + j * 6 * PAC_HALFN;
+    // (branch-free: an L/R line loads M/S-plane values it does not use, so no
+    // load waits inside a branch); the MLD pair arrives as MLD_M, MLD_S
     double t4[4][4];
+    int ms4[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = i * 256 + tid;
+        ms4[i] = l < lend ? (int)((msm >> bl4[i]) & 1u) : 0;
         const double* tp = thr + (ms4[i] ? 2 * PAC_HALFN : 0) + l;
         t4[i][0] = tp[0];
         t4[i][1] = tp[PAC_HALFN];
-        t4[i][2] = t4[i][3] = 0.0;
-        if (ms4[i]) {
-            const double mld = sh ? T->mld_s[l >> 2] : T->mld[l];
-            t4[i][2] = __dmul_rn(tp[2 * PAC_HALFN], mld);
-            t4[i][3] = __dmul_rn(tp[3 * PAC_HALFN], mld);
-        }
+        t4[i][2] = tp[2 * PAC_HALFN];
+        t4[i][3] = tp[3 * PAC_HALFN];
     }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     lds_sync();
@@ -812,7 +818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         double d0, d1;
         if (ms) {
             const double bM = t4[i][0], bS = t4[i][1];
-            const double mldM = t4[i][2], mldS = t4[i][3];
+            const double mldM = t4[i][2], mldS = t4[i][3];   // MLD_M, MLD_S
             const double a = bS < mldS ? bS : mldS;        // np.minimum(BTHR_S, MLD_S)
             const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
             const double c = bM < mldM ? bM : mldM;

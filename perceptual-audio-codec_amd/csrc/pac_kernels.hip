@@ -115,6 +115,14 @@ __device__ __forceinline__ double2 stereo_frame(const BlockPcm& r, int i) {
     return make_double2(pac_pcm_to_float((int)(int16_t)(w & 0xffffu)), pac_pcm_to_float((int)(int16_t)(w >> 16)));
 }
 
+// sample i of channel u (0, 1) of a stereo block (r: the channel-0 BlockPcm of
+// an interleaved stereo source): one 16-bit load; zero outside the stream
+__device__ __forceinline__ double stereo_sample(const BlockPcm& r, int i, int u) {
+    int c = 0;
+    if (i >= r.ilo && i < r.ihi) c = r.p[2 * (i - r.ilo) + u];
+    return pac_pcm_to_float(c);
+}
+
 // xs[i] = x(i) * sine[i] (window.py:27-39, codec.py:240) into LDS, i < 2048
 template <int NT>
 __device__ __forceinline__ void grp_stage_sine(const BlockRef& r, const PacTables* __restrict__ T,

@@ -444,14 +444,7 @@ template <int NT, bool NYQ = false, class D4>
 __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
                                                     double2* bufA, double2* bufB, int tid,
                                                     double* nyq = nullptr) {   // nyq: thread 0's
-#pragma unroll 4
-    for (int n0 = 0; n0 < 1024; n0 += NT) {
-        const int n = n0 + tid;
-        const double4 v = d4(n);
-        bufA[n] = make_double2(v.x, v.y);
-        bufB[n] = make_double2(v.z, v.w);
-    }
-    grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid);
+    grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid, d4);   // the staged pairs straight from d4
 #pragma unroll
     for (int p0 = 0; p0 < 512; p0 += NT) {
         const int p = p0 + tid;
@@ -742,16 +735,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid);
     } else if (st) {   // both channels' MDCTs stage by stage together
         if (!rL.f) {
-            grp_mdct2<256>([&](int i) {
-                const double2 x = stereo_frame(rL, i);
-                const double w = T->sine[i];
-                return make_double2(__dmul_rn(x.x, w), __dmul_rn(x.y, w));
-            }, T, bufA, bufB, tid);
+            grp_mdct2<256>([&](int i, int u) { return __dmul_rn(stereo_sample(rL, i, u), T->sine[i]); },
+                           T, bufA, bufB, tid);
         } else {
-            grp_mdct2<256>([&](int i) {
-                const double w = T->sine[i];
-                return make_double2(__dmul_rn(rL(i), w), __dmul_rn(rR(i), w));
-            }, T, bufA, bufB, tid);
+            grp_mdct2<256>([&](int i, int u) { return __dmul_rn(u ? rR(i) : rL(i), T->sine[i]); },
+                           T, bufA, bufB, tid);
         }
         XL = reinterpret_cast<const double*>(bufA);
         XR = reinterpret_cast<const double*>(bufB);

@@ -287,9 +287,13 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
 // Two independent one-buffer Stockham FFTs (buffers a and b) advanced stage by
 // stage together: each thread's butterflies of both in flight, one pair of
 // barriers per stage for both.  Bit-identical to grp_fft_stockham_1buf on each.
-template <int LOG, int NT>
+// The first stage takes its inputs from ld(n) = (a[n], b[n]) as a double4
+// (the staged sample pairs, computed from global memory) instead of LDS: no
+// staging pass and no first-stage barriers (the caller guarantees that no
+// thread still reads a or b).
+template <int LOG, int NT, class LD>
 __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b, const double2* __restrict__ tw,
-                                                         int tid) {
+                                                         int tid, const LD& ld) {
     constexpr int N = 1 << LOG;
     constexpr int N4 = N / 4;
     static_assert(N4 % NT == 0 && !(LOG & 1), "one radix-4 butterfly set per thread and stage");
@@ -299,27 +303,35 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
     for (int st = 0; st < LOG / 2; ++st) {
         const int Ns = 1 << (2 * st);
         double2 v[2][J][4];
-        grp_sync<NT>();
+        if (st == 0) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+            for (int q = 0; q < J; ++q)
 #pragma unroll
-            for (int q = 0; q < J; ++q) {
-                const int j = q * NT + tid;
-                const int k = j & (Ns - 1);
-                const bool swi = st > 0;
-                const int xj = swi ? fft_swz(j) : 0;
-                v[u][q][0] = bufs[u][j ^ xj];
-                v[u][q][1] = bufs[u][(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
-                v[u][q][2] = bufs[u][(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
-                v[u][q][3] = bufs[u][(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
-                if (Ns > 1) {
+                for (int i = 0; i < 4; ++i) {
+                    const double4 x = ld(q * NT + tid + i * N4);
+                    v[0][q][i] = make_double2(x.x, x.y);
+                    v[1][q][i] = make_double2(x.z, x.w);
+                }
+        } else {
+            grp_sync<NT>();
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int q = 0; q < J; ++q) {
+                    const int j = q * NT + tid;
+                    const int k = j & (Ns - 1);
+                    const int xj = fft_swz(j);
+                    v[u][q][0] = bufs[u][j ^ xj];
+                    v[u][q][1] = bufs[u][(j + N4) ^ xj ^ fft_swz(N4)];
+                    v[u][q][2] = bufs[u][(j + 2 * N4) ^ xj ^ fft_swz(2 * N4)];
+                    v[u][q][3] = bufs[u][(j + 3 * N4) ^ xj ^ fft_swz(3 * N4)];
                     const int e = k * (256 / Ns);
                     v[u][q][1] = cmul(v[u][q][1], tw[e]);
                     v[u][q][2] = cmul(v[u][q][2], tw[2 * e]);
                     v[u][q][3] = cmul(v[u][q][3], tw[3 * e]);
                 }
-            }
-        grp_sync<NT>();
+            grp_sync<NT>();
+        }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -343,75 +355,77 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
     grp_sync<NT>();
 }
 
-// Two independent ping-pong Stockham FFTs (src/dst pairs a, b) advanced stage
-// by stage together: one barrier per stage for both, bit-identical to
-// grp_fft_stockham on each.  Returns the result buffer of a (the one of b is
-// the matching buffer of its pair).
-template <int LOG, int NT>
-__device__ __forceinline__ void grp_fft_stockham_x2(double2* sa, double2* da, double2* sb, double2* db,
-                                                    const double2* __restrict__ tw, int tid,
-                                                    double2** ra, double2** rb) {
+// Two independent ping-pong Stockham FFTs (src/dst pairs a, b) of N = 2^LOG
+// points, LOG odd, N4 = N/4 = NT/2 (a 512-point pair on 256 threads), stage by
+// stage together (one barrier per stage for both, bit-identical to
+// grp_fft_stockham on each); returns the result buffers of a and b.  The
+// radix-4 stages split the threads, not the butterflies --
+// threads [0, N4) run FFT a, [N4, NT) FFT b, one butterfly each (no idle
+// half-workgroup) -- and the first stage takes its inputs from ld(n, u)
+// (element n of FFT u, computed from global memory) instead of LDS: no
+// staging pass, no first-stage barrier.
+template <int LOG, int NT, class LD>
+__device__ __forceinline__ void grp_fft_stockham_x2_ld(double2* sa, double2* da, double2* sb, double2* db,
+                                                       const double2* __restrict__ tw, int tid, const LD& ld,
+                                                       double2** ra, double2** rb) {
     constexpr int N = 1 << LOG;
     constexpr int N4 = N / 4;
+    static_assert(2 * N4 == NT && (LOG & 1), "a 2^odd pair split over the workgroup");
+    const int u = tid / N4, j = tid % N4;           // u wave-uniform (N4 a multiple of the wave)
 #pragma unroll
     for (int st = 0; st < LOG / 2; ++st) {
         const int Ns = 1 << (2 * st);
-        grp_sync<NT>();
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const double2* src = u ? sb : sa;
-            double2* dst = u ? db : da;
-#pragma unroll
-            for (int j0 = 0; j0 < N4; j0 += NT) {
-                const int j = j0 + tid;
-                if (N4 % NT != 0 && j >= N4) break;
-                const int k = j & (Ns - 1);
-                const bool swi = st > 0, swo = st + 1 < LOG / 2 || (LOG & 1);
-                const int xj = swi ? fft_swz(j) : 0;
-                double2 v0 = src[j ^ xj], v1 = src[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
-                double2 v2 = src[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
-                double2 v3 = src[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
-                if (Ns > 1) {
-                    const int e = k * (256 / Ns);
-                    v1 = cmul(v1, tw[e]);
-                    v2 = cmul(v2, tw[2 * e]);
-                    v3 = cmul(v3, tw[3 * e]);
-                }
-                const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
-                const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
-                const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
-                const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);
-                const int o = ((j - k) << 2) + k;
-                const int xo = swo ? fft_swz(o) : 0;
-                dst[o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
-                dst[(o + Ns) ^ xo ^ (swo ? fft_swz(Ns) : 0)] = make_double2(a1.x + a3.x, a1.y + a3.y);
-                dst[(o + 2 * Ns) ^ xo ^ (swo ? fft_swz(2 * Ns) : 0)] = make_double2(a0.x - a2.x, a0.y - a2.y);
-                dst[(o + 3 * Ns) ^ xo ^ (swo ? fft_swz(3 * Ns) : 0)] = make_double2(a1.x - a3.x, a1.y - a3.y);
-            }
+        const double2* src = u ? sb : sa;
+        double2* dst = u ? db : da;
+        const int k = j & (Ns - 1);
+        double2 v0, v1, v2, v3;
+        if (st == 0) {
+            v0 = ld(j, u);
+            v1 = ld(j + N4, u);
+            v2 = ld(j + 2 * N4, u);
+            v3 = ld(j + 3 * N4, u);
+        } else {
+            grp_sync<NT>();
+            const int xj = fft_swz(j);
+            v0 = src[j ^ xj];
+            v1 = src[(j + N4) ^ xj ^ fft_swz(N4)];
+            v2 = src[(j + 2 * N4) ^ xj ^ fft_swz(2 * N4)];
+            v3 = src[(j + 3 * N4) ^ xj ^ fft_swz(3 * N4)];
+            const int e = k * (256 / Ns);
+            v1 = cmul(v1, tw[e]);
+            v2 = cmul(v2, tw[2 * e]);
+            v3 = cmul(v3, tw[3 * e]);
         }
+        const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
+        const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
+        const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
+        const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);
+        const int o = ((j - k) << 2) + k;
+        const int xo = fft_swz(o);                  // LOG odd: every radix-4 stage writes swizzled
+        dst[o ^ xo] = make_double2(a0.x + a2.x, a0.y + a2.y);
+        dst[(o + Ns) ^ xo ^ fft_swz(Ns)] = make_double2(a1.x + a3.x, a1.y + a3.y);
+        dst[(o + 2 * Ns) ^ xo ^ fft_swz(2 * Ns)] = make_double2(a0.x - a2.x, a0.y - a2.y);
+        dst[(o + 3 * Ns) ^ xo ^ fft_swz(3 * Ns)] = make_double2(a1.x - a3.x, a1.y - a3.y);
         double2* t = sa; sa = da; da = t;
         t = sb; sb = db; db = t;
     }
-    if (LOG & 1) {
-        grp_sync<NT>();
+    grp_sync<NT>();                                 // last stage, radix 2, Ns = N/2
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const double2* src = u ? sb : sa;
-            double2* dst = u ? db : da;
+    for (int w = 0; w < 2; ++w) {
+        const double2* src = w ? sb : sa;
+        double2* dst = w ? db : da;
 #pragma unroll
-            for (int j0 = 0; j0 < N / 2; j0 += NT) {
-                const int j = j0 + tid;
-                if ((N / 2) % NT != 0 && j >= N / 2) break;
-                const int xj = fft_swz(j);
-                const double2 v0 = src[j ^ xj];
-                const double2 v1 = cmul(src[(j + N / 2) ^ xj ^ fft_swz(N / 2)], tw[j * (1024 / N)]);
-                dst[j] = make_double2(v0.x + v1.x, v0.y + v1.y);
-                dst[j + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
-            }
+        for (int j0 = 0; j0 < N / 2; j0 += NT) {
+            const int jj = j0 + tid;
+            const int xj = fft_swz(jj);
+            const double2 v0 = src[jj ^ xj];
+            const double2 v1 = cmul(src[(jj + N / 2) ^ xj ^ fft_swz(N / 2)], tw[jj * (1024 / N)]);
+            dst[jj] = make_double2(v0.x + v1.x, v0.y + v1.y);
+            dst[jj + N / 2] = make_double2(v0.x - v1.x, v0.y - v1.y);
         }
-        double2* t = sa; sa = da; da = t;
-        t = sb; sb = db; db = t;
     }
+    double2* t = sa; sa = da; da = t;
+    t = sb; sb = db; db = t;
     grp_sync<NT>();
     *ra = sa;
     *rb = sb;
@@ -465,30 +479,31 @@ __device__ __forceinline__ double* grp_mdct(const XS& xs, const PacTables* __res
     return X;
 }
 
-// Two MDCTs at once (grp_mdct of xa into bufA and of xb into bufB, FFTs
-// stage by stage together; xab(i) = (xa(i), xb(i)) so a stereo source loads
-// each frame once): bit-identical to two grp_mdct calls.
-template <int NT, class FAB>
-__device__ __forceinline__ void grp_mdct2(const FAB& xab, const PacTables* __restrict__ T,
+// Two MDCTs at once (grp_mdct of channel 0 into bufA and of channel 1 into
+// bufB, FFTs stage by stage together; xu(i, u) = windowed sample i of channel
+// u): bit-identical to two grp_mdct calls.
+template <int NT, class XU>
+__device__ __forceinline__ void grp_mdct2(const XU& xu, const PacTables* __restrict__ T,
                                           double2* bufA, double2* bufB, int tid) {
-    // xab(i) = (xa(i), xb(i)): the two windowed samples at i
-    auto fold = [&](int n) {
-        if (n < 512) {
-            const double2 u = xab(1535 - n), w = xab(1536 + n);
-            return make_double2(__dsub_rn(-u.x, w.x), __dsub_rn(-u.y, w.y));
-        }
-        const double2 u = xab(n - 512), w = xab(1535 - n);
-        return make_double2(__dsub_rn(u.x, w.x), __dsub_rn(u.y, w.y));
+    auto fold = [&](int n, int u) {
+        if (n < 512) return __dsub_rn(-xu(1535 - n, u), xu(1536 + n, u));
+        return __dsub_rn(xu(n - 512, u), xu(1535 - n, u));
     };
+    double2 *Ya, *Yb;
+    // staged by every thread for both channels (one load per sample; feeding
+    // the first stage directly from global memory was slower here: each
+    // thread of the split stages would load its own channel's samples, twice
+    // the loads, and spilled)
 #pragma unroll
     for (int q0 = 0; q0 < 512; q0 += NT) {
         const int q = q0 + tid;
-        const double2 f0 = fold(2 * q), f1 = fold(1023 - 2 * q);
-        bufA[q] = cmul(make_double2(f0.x, f1.x), T->mdct_pre[q]);
-        bufB[q] = cmul(make_double2(f0.y, f1.y), T->mdct_pre[q]);
+        const double2 pq = T->mdct_pre[q];
+        bufA[q] = cmul(make_double2(fold(2 * q, 0), fold(1023 - 2 * q, 0)), pq);
+        bufB[q] = cmul(make_double2(fold(2 * q, 1), fold(1023 - 2 * q, 1)), pq);
     }
-    double2 *Ya, *Yb;
-    grp_fft_stockham_x2<9, NT>(bufA, bufA + 512, bufB, bufB + 512, T->fft_tw, tid, &Ya, &Yb);   // = buf + 512
+    grp_sync<NT>();
+    grp_fft_stockham_x2_ld<9, NT>(bufA, bufA + 512, bufB, bufB + 512, T->fft_tw, tid,
+                                  [&](int n, int u) { return (u ? bufB : bufA)[n]; }, &Ya, &Yb);
     double* XA = reinterpret_cast<double*>(bufA);
     double* XB = reinterpret_cast<double*>(bufB);
 #pragma unroll

@@ -439,12 +439,15 @@ __device__ __forceinline__ void grp_spectrum_cplx(const DS& d, const PacTables* 
 
 // the complex spectra of two real 2048-blocks dA, dB at once (as
 // grp_spectrum_cplx on each: bit-identical), both FFTs stage by stage together
-// (d4(n) = (dA(2n), dA(2n+1), dB(2n), dB(2n+1)): the staged pairs of both)
-template <int NT, bool NYQ = false, class D4>
-__device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
-                                                    double2* bufA, double2* bufB, int tid,
-                                                    double* nyq = nullptr) {   // nyq: thread 0's
-    grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid, d4);   // the staged pairs straight from d4
+// (d4(n) = (dA(2n), dA(2n+1), dB(2n), dB(2n+1)): the staged pairs of both, fed
+// straight into the first stage).  The real split hands every bin to
+// put(u, k, X[k]) (u = 0: A, 1: B; k < 1024, and the real Nyquist bin k = 1024
+// = sum_even - sum_odd); thread p computes its own bin pair p, 1024 - p from
+// the pair's two FFT values only, so put may write them back in place.
+template <int NT, class D4, class PUT>
+__device__ __forceinline__ void grp_spectrum_cplx2p_put(const D4& d4, const PacTables* __restrict__ T,
+                                                        double2* bufA, double2* bufB, int tid, const PUT& put) {
+    grp_fft_stockham_1buf_x2<10, NT>(bufA, bufB, T->fft_tw, tid, d4);
 #pragma unroll
     for (int p0 = 0; p0 < 512; p0 += NT) {
         const int p = p0 + tid;
@@ -453,7 +456,7 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
         kk[1] = p ? 1024 - p : 512;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            double2* Z = u ? bufB : bufA;
+            const double2* Z = u ? bufB : bufA;
             double2 X[2];
 #pragma unroll
             for (int side = 0; side < 2; ++side) {
@@ -464,11 +467,19 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
                 const double2 wo = cmul(T->rfft_tw[kk[side]], o);
                 X[side] = make_double2(e.x + wo.y, e.y - wo.x);
             }
-            if (NYQ && p == 0) nyq[u] = Z[0].x - Z[0].y;   // X[1024] = sum_even - sum_odd
-            Z[kk[0]] = X[0];
-            Z[kk[1]] = X[1];
+            if (p == 0) put(u, 1024, make_double2(Z[0].x - Z[0].y, 0.0));
+            put(u, kk[0], X[0]);
+            put(u, kk[1], X[1]);
         }
     }
+}
+// ... with the spectra left in place in bufA, bufB (bins 0..1023)
+template <int NT, class D4>
+__device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTables* __restrict__ T,
+                                                    double2* bufA, double2* bufB, int tid) {
+    grp_spectrum_cplx2p_put<NT>(d4, T, bufA, bufB, tid, [&](int u, int k, double2 X) {
+        if (k < 1024) (u ? bufB : bufA)[k] = X;
+    });
     grp_sync<NT>();
 }
 
@@ -599,15 +610,24 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
                                            const PacMasterChunkBuf& K, const PacMasterFields& F,
                                            const PacMasterChunk& ck, const ChunkPos& cp, int64_t j, double2* bufA,
                                            double2* bufB) {
-    double nyq[2] = {0.0, 0.0};   // thread 0's registers (the split's pair p = 0): 32 KB LDS, 5 WG/CU
     const int tid = threadIdx.x;
     const int64_t gb = cp.gb;
     const int fl = F.bsf ? F.bsf[gb] : 0;
     if (fl & PAC_BS_SHORT) return;                 // k_master_thr_short's
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // mono: B = A, unused
+    // bins -2..1026 at o[bin + 2], written by the real split straight from its
+    // registers (no LDS round trip): the mirrored edge bins X[-k] = X[2048-k] =
+    // conj X[k] stored too, so the taps of k_master_thr need no index arithmetic
+    double2* o = K.spec + j * 2 * PAC_SPEC_LD + 2;
+    auto put = [&](int u, int k, double2 X) {
+        double2* q = o + u * PAC_SPEC_LD;
+        q[k] = X;
+        if (k == 1 || k == 2) q[-k] = make_double2(X.x, -X.y);
+        if (k == 1022 || k == 1023) q[2048 - k] = make_double2(X.x, -X.y);
+    };
     if (ck.nch == 2 && !rL.f) {
-        grp_spectrum_cplx2p<256, true>([&](int n) {   // frames 2n, 2n+1 of both channels, one load each
+        grp_spectrum_cplx2p_put<256>([&](int n) {   // frames 2n, 2n+1 of both channels, one load each
             const int i0 = 2 * n;
             const double2 f0 = stereo_frame(rL, i0), f1 = stereo_frame(rL, i0 + 1);
             const double2 h = *reinterpret_cast<const double2*>(T->hann + i0);
@@ -615,34 +635,14 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
                                  : *reinterpret_cast<const double2*>(T->sine + i0);
             return make_double4(__dmul_rn(__dmul_rn(f0.x, w.x), h.x), __dmul_rn(__dmul_rn(f1.x, w.y), h.y),
                                 __dmul_rn(__dmul_rn(f0.y, w.x), h.x), __dmul_rn(__dmul_rn(f1.y, w.y), h.y));
-        }, T, bufA, bufB, tid, nyq);
+        }, T, bufA, bufB, tid, put);
     } else {
-        grp_spectrum_cplx2p<256, true>([&](int n) {
+        grp_spectrum_cplx2p_put<256>([&](int n) {
             return make_double4(variant_sample(rL, rR, T, 0, 2 * n, fl), variant_sample(rL, rR, T, 0, 2 * n + 1, fl),
                                 variant_sample(rL, rR, T, 1, 2 * n, fl), variant_sample(rL, rR, T, 1, 2 * n + 1, fl));
-        }, T, bufA, bufB, tid, nyq);
+        }, T, bufA, bufB, tid, put);
     }
     MPROF(3);
-    // bins -2..1026 at o[bin + 2]: the mirrored edge bins X[-k] = X[2048-k] =
-    // conj X[k] stored, so the taps of k_master_thr need no index arithmetic
-    double2* o = K.spec + j * 2 * PAC_SPEC_LD + 2;
-#pragma unroll
-    for (int k = tid; k < 1024; k += 256) {
-        o[k] = bufA[k];
-        o[PAC_SPEC_LD + k] = bufB[k];
-    }
-    if (tid == 0) {                                // bins 1024 (Nyquist, real), -1, -2, 1025, 1026
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const double2* X = u ? bufB : bufA;
-            double2* q = o + u * PAC_SPEC_LD;
-            q[1024] = make_double2(nyq[u], 0.0);
-            q[-1] = make_double2(X[1].x, -X[1].y);
-            q[-2] = make_double2(X[2].x, -X[2].y);
-            q[1025] = make_double2(X[1023].x, -X[1023].y);
-            q[1026] = make_double2(X[1022].x, -X[1022].y);
-        }
-    }
     MPROF(4);
 }
 

@@ -802,6 +802,26 @@ __device__ __forceinline__ void grp_scan_lists(const MaskerLists& L, int tid) {
     grp_sync<NT>();
 }
 
+// Exclusive prefix of the A*NW segment counts c[i] (segment i = a * NW + w:
+// bin-order chunks of the NW waves): lanes 0..A*NW-1 scan them by DPP row
+// shifts inside one 16-lane row, and each wave reads its own A entries by
+// readlane -- instead of every thread summing all of them serially.
+template <int A, int NW>
+__device__ __forceinline__ void seg_prefix(const int* c, int lane, int w, int (&out)[A], int* total) {
+    static_assert(A * NW <= 16, "one DPP row");
+    const int v = lane < A * NW ? c[lane] : 0;
+    int s = v;
+    s += __builtin_amdgcn_update_dpp(0, s, PAC_DPP_SHR(1), 0xf, 0xf, false);
+    s += __builtin_amdgcn_update_dpp(0, s, PAC_DPP_SHR(2), 0xf, 0xf, false);
+    s += __builtin_amdgcn_update_dpp(0, s, PAC_DPP_SHR(4), 0xf, 0xf, false);
+    s += __builtin_amdgcn_update_dpp(0, s, PAC_DPP_SHR(8), 0xf, 0xf, false);
+    const int ex = s - v;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+    for (int a = 0; a < A; ++a) out[a] = __builtin_amdgcn_readlane(ex, a * NW + wu);
+    *total = __builtin_amdgcn_readlane(s, 15);
+}
+
 // findpeaks (psychoac.py:158-191) on |X|^2 held in pw[k] (the floor
 // 10 log10|X| > -30 is the equivalent |X|^2 > T->peak_floor2), masker SPL from the
 // 6-bin slice X[k-3:k+3] (psychoac.py:448, Python slice semantics), then the
@@ -831,14 +851,13 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
         if (lane == 0) cnt[j * NW + w] = __popcll(bal[j]);
     }
     grp_sync<NT>();
-    int pre[J * NW];                 // exclusive prefix of the segment counts
-    int tot = 0;
-#pragma unroll
-    for (int i = 0; i < J * NW; ++i) { pre[i] = tot; tot += cnt[i]; }
+    int tot;
+    int pj[J];                       // exclusive prefix of this wave's segment counts
+    seg_prefix<J, NW>(cnt, lane, w, pj, &tot);
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        const int idx = pre[j * NW + w] + __popcll(bal[j] & below);
+        const int idx = pj[j] + __popcll(bal[j] & below);
         L.rank[j * NT + tid] = (int16_t)idx;
         if ((bal[j] >> lane) & 1ull) kidx[idx] = j * NT + tid;
     }
@@ -876,10 +895,9 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
         if (lane == 0) cnt2[q * NW + w] = __popcll(lb[q]);
     }
     grp_sync<NT>();   // every |X|^2 read done before the lists overwrite buf; loud counts visible
-    int pre2[R * NW];
-    int nloud = 0;
-#pragma unroll
-    for (int i = 0; i < R * NW; ++i) { pre2[i] = nloud; nloud += cnt2[i]; }
+    int nloud;
+    int pq[R];                       // exclusive prefix of this wave's loud counts
+    seg_prefix<R, NW>(cnt2, lane, w, pq, &nloud);
 #pragma unroll
     for (int q = 0; q < R; ++q) {           // R * NT = 512: every slot, zero past nm
         const int idx = q * NT + tid;
@@ -888,7 +906,7 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
         L.sl[pi] = rPL[q];
         L.su[pi] = rPU[q];
         if (idx < tot) {
-            const int j = pre2[q * NW + w] + __popcll(lb[q] & below);
+            const int j = pq[q] + __popcll(lb[q] & below);
             L.lpre[idx] = (int16_t)j;
             if ((lb[q] >> lane) & 1ull) { L.lz[j] = rz[q]; L.lB[j] = rB[q]; L.lku[j] = rku[q]; }
         }

@@ -172,11 +172,7 @@ __device__ __forceinline__ void wave_threshold_short(char* R, const PacTables* _
         z[h] = B[h] = ku[h] = E[h] = P[h] = Q[h] = 0.0;
         if (m < nm) {
             const int k = kidx[m];
-            double s = 0.0;
-            if (k >= 3) {
-                const int hi = k + 3 < 256 ? k + 3 : 256;
-                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, pw[i]);
-            }
+            const double s = slice6_sum(pw, k, 256);
             const double sp = pac_spl(csp * s);
             double lev = sp - 40.0;
             lev = 0.367 * (0.0 > lev ? 0.0 : lev);

@@ -802,6 +802,19 @@ __device__ __forceinline__ void grp_scan_lists(const MaskerLists& L, int tid) {
     grp_sync<NT>();
 }
 
+// sum(|X[k-3:k+3]|^2) of a peak bin k (psychoac.py:448: Python slice
+// semantics -- empty for k < 3, cut at the spectrum's end n -- and the builtin
+// sum from 0 in bin order) as six independent LDS reads; a peak has k <= n-2,
+// so only the sixth bin can fall past the end (it is read, in bounds of the
+// caller's buffer, and not added)
+__device__ __forceinline__ double slice6_sum(const double* pw, int k, int n) {
+    if (k < 3) return 0.0;
+    const double* q = pw + (k - 3);
+    const double a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+    const double s = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(a, b), c), d), e);
+    return k + 2 < n ? __dadd_rn(s, f) : s;
+}
+
 // Exclusive prefix of the A*NW segment counts c[i] (segment i = a * NW + w:
 // bin-order chunks of the NW waves): lanes 0..A*NW-1 scan them by DPP row
 // shifts inside one 16-lane row, and each wave reads its own A entries by
@@ -874,11 +887,7 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
         rz[q] = rB[q] = rku[q] = rE[q] = rPL[q] = rPU[q] = 0.0;
         if (idx < tot) {
             const int k = kidx[idx];
-            double s = 0.0;
-            if (k >= 3) {
-                const int hi = k + 3 < 1024 ? k + 3 : 1024;
-                for (int i = k - 3; i < hi; ++i) s = __dadd_rn(s, pw[i]);   // builtin sum, from 0
-            }
+            const double s = slice6_sum(pw, k, 1024);
             const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
             const double sp = pac_spl(csp * s);
             double lev = sp - 40.0;

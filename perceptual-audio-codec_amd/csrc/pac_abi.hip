@@ -152,6 +152,16 @@ static void build_tables(int fs, int window, PacTables* t) {
         double a = -2.0 * M_PI * k / 2048.0;
         t->rfft_tw[k] = make_double2(cos(a), sin(a));
     }
+    t->sine_win = window == PAC_WINDOW_SINE;
+    for (int k = 0; k < PAC_HALFN; k++) {
+        // sin(pi (n + 1/2)/N) = (e^{i pi (n+1/2)/N} - e^{-i pi (n+1/2)/N}) / 2i turns the
+        // MDCT's odd-frequency sum of x*w into (c X[k] - conj(c) X[k+1]) / 2i, c = e^{i pi/2N}
+        const long double pi = 3.141592653589793238462643383279502884L;
+        const long double th = 2.0L * pi * 512.5L * ((long double)k + 0.5L) / 2048.0L;
+        const long double a = th - pi / 4096.0L, b = th + pi / 4096.0L;
+        t->mdct_tw2[k] = make_double4((double)(cosl(a) / 2048.0L), (double)(sinl(a) / 2048.0L),
+                                      (double)(cosl(b) / 2048.0L), (double)(sinl(b) / 2048.0L));
+    }
     {   // mdct.py:355 post-twiddle angle, evaluated as numpy does
         double c1 = (-2.0 * M_PI) / (double)PAC_N;
         double c2 = c1 * 512.5;
@@ -321,6 +331,7 @@ struct pac_ctx {
     // master
     DevBuf<double> m_thr, m_lines, m_smr, m_peak;
     DevBuf<double2> m_spec;               // [chunk][2][PAC_SPEC_LD] k_master_spec -> k_master_thr
+    DevBuf<double> m_mdct;                // [2][chunk][2][1024] side kernel -> k_master_front<true>
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
     DevBuf<uint32_t> m_rowm;                // [nblocks] k_master_lrms -> k_master_thr row masks
     DevBuf<uint32_t> m_msm;                 // [nblocks] k_master_lrms -> k_master_front LRMS band masks
@@ -346,6 +357,7 @@ struct pac_ctx {
     bool tail_serial = false;
     int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
     bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
+    bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -390,6 +402,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_TAIL_MODE")) c->tail_serial = !strcmp(f, "serial");
     if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
+    if (const char* f = getenv("PAC_FRONT_FAST")) c->front_fast = atoi(f) != 0;
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -419,7 +432,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->m_stg_next.release();
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
-    c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release();
+    c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release(); c->m_mdct.release();
     c->m_lrms.release(); c->m_rowm.release(); c->m_msm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->m_perm.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
@@ -880,6 +893,10 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipGetLastError());
         F.bsf = c->bs_fl.p;
     }
+    // the MDCT lines from the side kernel's LRMS spectra (mdct_from_dft): sine
+    // window, stereo, no block switching; otherwise the front transforms
+    const bool front_fast = c->front_fast && nch == 2 && !F.bsf && p->window == PAC_WINDOW_SINE && c->side_fused;
+    if (front_fast && (rc = c->m_mdct.ensure(2 * cbmax * 2 * PAC_HALFN))) return rc;
     if (dbg_codes) {
         if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
             (rc = c->dbg_len.ensure(G * PAC_HALFN)))
@@ -933,17 +950,20 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         const int64_t k = i % 3;
         return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
-                                 c->m_spec.p, c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN};
+                                 c->m_spec.p, c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
+                                 front_fast ? c->m_mdct.p + (i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
     };
     // PAC_DEBUG_FLAGS 32: phase clocks of the fused LRMS + spectra kernel, 64: of the front
-    PacSource src_side = src, src_front = src;
+    // 128: of the thresholds
+    PacSource src_side = src, src_front = src, src_thr = src;
     const int64_t nprof = (int64_t)PAC_PROF_WG * 4 * PAC_PROF_MARKS;
-    if (c->dbg & (32 | 64)) {
+    if (c->dbg & (32 | 64 | 128)) {
         if ((rc = c->prof.ensure(nprof))) return rc;
         HIPCHK(hipMemsetAsync(c->prof.p, 0, nprof * sizeof(long long), s0));
         HIPCHK(hipStreamWaitEvent(s2, event_on(s0), 0));
         if (c->dbg & 32) src_side.prof = c->prof.p;
-        else src_front.prof = c->prof.p;
+        else if (c->dbg & 64) src_front.prof = c->prof.p;
+        else src_thr.prof = c->prof.p;
     }
     auto launch_side = [&](int64_t i) -> int {         // lrms(i), spec(i) on s2
         int rc2;
@@ -971,8 +991,8 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
         if (i >= 3) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
         if ((rc = mark(0, -1))) return rc;
-        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0, src,
-                           T, K, F, q.ck);
+        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0,
+                           src_thr, T, K, F, q.ck);
         if ((rc = mark(0, 0))) return rc;
         if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
             hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(q.B * nvar)), dim3(256), 0, s0, src, T, K, F,
@@ -986,7 +1006,10 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             spec_ready = event_on(s2);
         }
         if ((rc = mark(0, -1))) return rc;
-        hipLaunchKernelGGL(k_master_front, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
+        if (front_fast)
+            hipLaunchKernelGGL(k_master_front<true>, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
+        else
+            hipLaunchKernelGGL(k_master_front<false>, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
         HIPCHK(hipGetLastError());
         if ((rc = mark(0, 1))) return rc;
         // the tail of this chunk once the next chunk's spectra are ready too,
@@ -1018,7 +1041,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     }
     HIPCHK(hipStreamWaitEvent(s0, event_on(s1), 0));
     HIPCHK(hipStreamWaitEvent(s0, event_on(s3), 0));
-    if (c->dbg & (32 | 64)) {
+    if (c->dbg & (32 | 64 | 128)) {
         HIPCHK(hipStreamWaitEvent(s0, event_on(s2), 0));
         if ((rc = report_phase_clocks(c, s0, nprof))) return rc;
     }

@@ -19,6 +19,10 @@ struct PacTables {
     double hann[PAC_N];           // window.py:41-53
     double2 mdct_pre[PAC_HALFN / 2];   // exp(-i pi (q+1/4)/M)   (DCT-IV fold, M=1024)
     double2 mdct_post[PAC_HALFN / 2];  // exp(-i pi q / M)
+    // MDCT line k of the sine-windowed block from the raw block's DFT bins X[k],
+    // X[k+1] (k_master_lrms_spec, pac_master.hip mdct_from_dft):
+    // (cos a, sin a, cos b, sin b) / N, a, b = 2 pi n0 (k + 1/2)/N -+ pi/(2N)
+    double4 mdct_tw2[PAC_HALFN];
     double2 fft_tw[PAC_HALFN];         // exp(-2 pi i k / 1024), k < 1024
     double2 rfft_tw[PAC_HALFN];        // exp(-2 pi i k / 2048), k < 1024
     double bark_line[PAC_HALFN];  // Bark(MDCTFreqs)                psychoac.py:434,95
@@ -34,7 +38,7 @@ struct PacTables {
     // sign bit (quantize.py:333), so silent blocks depend on it.
     uint8_t mdct_zero_neg[PAC_HALFN];
     int32_t sample_rate;
-    int32_t pad_;
+    int32_t sine_win;             // 1: the MDCT window is the sine window (mdct_tw2 applies)
     // findpeaks floor 10 log10|X| > -30 (psychoac.py:168) as |X|^2 > peak_floor2:
     // the square of the largest double m with 10*log10(m) <= -30 (host libm)
     double peak_floor2;

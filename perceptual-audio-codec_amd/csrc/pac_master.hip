@@ -50,6 +50,10 @@ struct PacMasterChunkBuf {
     double* bandpeak;   // [Bc][2][25]    max |line| per band
     double2* spec;      // [Bc][2][PAC_SPEC_LD] FFT bins -2..1026 of a and b (k_master_spec)
     uint16_t* codes;    // [Bc][2][1024] signed mantissa codes, tail-internal (F.codes when the pack runs)
+    // [Bc][2][1024] the MDCT lines of L and R (sine window, plain long frames,
+    // stereo), computed by the side kernel from the LRMS spectra and read by the
+    // front (k_master_front<true>); null: the front transforms the block itself
+    double* mdct;
 };
 #define PAC_SPEC_LD 1040    // double2 per spectrum: bins -2..1026 at [bin + 2], padded to 256 B
 
@@ -185,14 +189,23 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
 
 // one threshold variant of a block (k_master_thr): |V|^2 from the block's
 // spectra, maskers, the rows the variant's bands use.
+// diagnostic (PAC_DEBUG_FLAGS 128): shader clock at phase mark k of every wave
+// (pm = this workgroup's marks, or null)
+#define TPROF(k)                                                                                     \
+    do {                                                                                             \
+        if (pm && (threadIdx.x & (WAVE - 1)) == 0)                                                   \
+            pm[(threadIdx.x / WAVE) * PAC_PROF_MARKS + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
 __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double2* __restrict__ spec,
                                          double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
-                                         int tid) {
+                                         int tid, long long* pm, int mk) {
     const int lane = tid & (WAVE - 1);
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
     grp_variant_pow<FRONT_NT>(spec, v, buf, tid);
+    TPROF(mk);
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(reinterpret_cast<const double*>(buf), T, v >= 4 ? 0.0 : 15.0, tid, L);
+    TPROF(mk + 1);
     // rows claimed dynamically, most expensive first (as in k_origin_front)
     int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
@@ -210,6 +223,7 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
         // the only form k_master_front reads
         out[r * WAVE + lane] = v >= 4 ? __dmul_rn(t, T->mld[r * WAVE + lane]) : t;
     }
+    TPROF(mk + 2);
 }
 
 // One workgroup per (block, variant pair) -- {0,1} = L/R, {2,3} = M/S,
@@ -247,12 +261,17 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     rows = __builtin_amdgcn_readfirstlane(rows);
     if (!rows) return;
     const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
-    thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid);
+    long long* pm = (src.prof && blockIdx.x < PAC_PROF_WG) ? src.prof + (int64_t)blockIdx.x * 4 * PAC_PROF_MARKS
+                                                          : nullptr;
+    TPROF(0);
+    thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
     if (ck.nch != 2) return;
     lds_sync();                                             // the first variant's lists are read
+    TPROF(4);
     int t2 = tid;                // opaque copy: no per-lane address of the first call is kept live for the second
     asm volatile("" : "+v"(t2));
-    thr_variant(T, spec, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2);
+    thr_variant(T, spec, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2, pm, 5);
+    TPROF(8);
 }
 
 // Block-switching extension (pac_bs.h): the thresholds of a SHORT frame.  One
@@ -487,9 +506,27 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
 // |sum(L^2 - R^2)| < 0.8 |sum(L^2 + R^2)| per band, over the complex FFT bins
 // of the raw (unwindowed) blocks, with numpy's pairwise sums.  It runs first so
 // that k_master_thr computes only the thresholds a band's coding mode uses.
+// MDCT line k (mdct.py:49-82, N = 2048, n0 = 512.5, 2/N forward) of the
+// sine-windowed block from the raw block's DFT X (the LRMS spectra): with
+// w[n] = sin(pi (n + 1/2)/N) = (e^{i pi (n+1/2)/N} - e^{-i pi (n+1/2)/N}) / 2i the
+// odd-frequency sum sum_n x w e^{-2 pi i n (k+1/2)/N} is (c X[k] - conj(c) X[k+1]) / 2i,
+// c = e^{i pi/2N}, so X_mdct[k] = Im(e^{-ia} X[k] - e^{-ib} X[k+1]) / N,
+// a, b = 2 pi n0 (k + 1/2)/N -+ pi/2N (T->mdct_tw2).  Mathematically the
+// reference's transform; rounding of the same class as an FFT's (the terms
+// are bounded by the raw spectrum's bins).  Exactly-zero lines take the
+// reference's signed zero.
+__device__ __forceinline__ double mdct_from_dft(double2 x0, double2 x1, const PacTables* __restrict__ T, int k) {
+    const double4 tw = T->mdct_tw2[k];
+    double r = x0.y * tw.x;
+    r = __builtin_fma(-x0.x, tw.y, r);
+    r = __builtin_fma(-x1.y, tw.z, r);
+    r = __builtin_fma(x1.x, tw.w, r);
+    return r == 0.0 ? (T->mdct_zero_neg[k] ? -0.0 : 0.0) : r;
+}
+
 __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables* __restrict__ T,
                                            const PacMasterFields& F, const ChunkPos& cp, double2* bufA,
-                                           double2* bufB) {
+                                           double2* bufB, double* __restrict__ mdct) {
     const int tid = threadIdx.x;
     const int64_t gb = cp.gb;
     const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
@@ -511,17 +548,36 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         lob = T->lower[tid];
     }
     MPROF(0);
+    // bins 0..1023 in place; the real Nyquist bins (thread 0) kept for the MDCT
+    double nyA = 0.0, nyB = 0.0;
+    auto put = [&](int u, int k, double2 X) {
+        if (k < 1024) (u ? bufB : bufA)[k] = X;
+        else if (u) nyB = X.x;
+        else nyA = X.x;
+    };
     if (!rL.f) {
-        grp_spectrum_cplx2p<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
+        grp_spectrum_cplx2p_put<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
             const double2 f0 = stereo_frame(rL, 2 * n), f1 = stereo_frame(rL, 2 * n + 1);
             return make_double4(f0.x, f1.x, f0.y, f1.y);
-        }, T, bufA, bufB, tid);
+        }, T, bufA, bufB, tid, put);
     } else {
-        grp_spectrum_cplx2p<256>([&](int n) {
+        grp_spectrum_cplx2p_put<256>([&](int n) {
             return make_double4(rL(2 * n), rL(2 * n + 1), rR(2 * n), rR(2 * n + 1));
-        }, T, bufA, bufB, tid);
+        }, T, bufA, bufB, tid, put);
     }
+    lds_sync();
     MPROF(1);
+    if (mdct) {        // the front's MDCT lines from these spectra; thread 0 owns line 1023
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = 1023 - 256 * i - tid;
+            const double2 a0 = bufA[k], b0 = bufB[k];
+            const double2 a1 = k == 1023 ? make_double2(nyA, 0.0) : bufA[k + 1];
+            const double2 b1 = k == 1023 ? make_double2(nyB, 0.0) : bufB[k + 1];
+            mdct[k] = mdct_from_dft(a0, a1, T, k);
+            mdct[PAC_HALFN + k] = mdct_from_dft(b0, b1, T, k);
+        }
+    }
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
@@ -598,7 +654,7 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    lrms_block(src, T, F, cp, bufA, bufB);
+    lrms_block(src, T, F, cp, bufA, bufB, nullptr);
 }
 
 // One 256-thread workgroup per stereo block: the complex spectra A = FFT(a),
@@ -663,7 +719,8 @@ __global__ __launch_bounds__(256) void k_master_lrms_spec(PacSource src, const P
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    if (ck.nch == 2) lrms_block(src, T, F, cp, bufA, bufB);
+    // K.mdct: set by the host only for sine-window stereo calls without block switching
+    if (ck.nch == 2) lrms_block(src, T, F, cp, bufA, bufB, K.mdct ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
     lds_sync();                                   // the leaf sums are read before the spectra overwrite them
     spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
 }
@@ -692,24 +749,25 @@ __device__ __forceinline__ void seg_max_step(unsigned long long& k0, unsigned lo
 // One 256-thread workgroup per stereo block: MDCT L/R and overall scales, M/S
 // lines, MLD threshold combination, SMR selection and the band maxima (LDS
 // atomic max on order-preserving keys).  Only the thresholds of each band's
-// coding mode are read (k_master_thr computes no others).
+// coding mode are read (k_master_thr computes no others).  FAST: a stereo
+// sine-window call without block switching, whose MDCT lines the side kernel
+// derived from the LRMS spectra (K.mdct): no transform here, 1.5 KB of LDS.
+template <bool FAST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_master_front(PacSource src, const PacTables* __restrict__ T,
                                                       PacMasterChunkBuf K, PacMasterFields F,
                                                       PacMasterChunk ck) {
-    __shared__ double2 bufA[1024], bufB[1024];    // 32 KB (5 workgroups per CU)
+    __shared__ double2 bufA[FAST ? 1 : 1024], bufB[FAST ? 96 : 1024];    // 32 KB (5 workgroups per CU) / 1.5 KB
     // after the MDCTs: SMR 0/1, |line| 0/1, max|X| L/R keys and the LRMS flags
     // in the free upper half of bufB
-    unsigned long long (*key)[32] = reinterpret_cast<unsigned long long (*)[32]>(bufB + 512);
+    unsigned long long (*key)[32] = reinterpret_cast<unsigned long long (*)[32]>(FAST ? bufB : bufB + 512);
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, j, &cp)) return;
     const int64_t gb = cp.gb;
-    const bool st = ck.nch == 2;                 // mono master: channel 0 alone, LRMS all 0
-    const int fl = F.bsf ? F.bsf[gb] : 0;        // block-switching flags (pac_bs.h), 0: off
+    const bool st = FAST || ck.nch == 2;         // mono master: channel 0 alone, LRMS all 0
+    const int fl = (!FAST && F.bsf) ? F.bsf[gb] : 0;   // block-switching flags (pac_bs.h), 0: off
     const bool sh = fl & PAC_BS_SHORT;
-    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
-    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
     // each thread's four lines l = 256 i + tid: bands, and the block's LRMS
     // band mask, loaded before the MDCT (no wait: the LDS barriers leave them
     // in flight) so that the threshold loads can all issue right after it
@@ -721,9 +779,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     MPROF(0);
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
-    const double* XL;
+    double xl4[4], xr4[4];
+    if constexpr (FAST) {
+        const double* md = K.mdct + j * 2 * PAC_HALFN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xl4[i] = md[i * 256 + tid];
+            xr4[i] = md[PAC_HALFN + i * 256 + tid];
+        }
+    }
+    const double* XL = nullptr;
     const double* XR = nullptr;
-    if (sh) {          // four short MDCTs per channel, interleaved (scratch: the buffers' upper halves)
+    if constexpr (FAST) {
+    } else if (sh) {
+        const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+        const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));          // four short MDCTs per channel, interleaved (scratch: the buffers' upper halves)
         double* xl = reinterpret_cast<double*>(bufA);
         double* xr = reinterpret_cast<double*>(bufB);
         grp_short_mdct(rL, T, bufA + 512, bufB + 512, xl, tid);
@@ -731,9 +801,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         XL = xl;
         XR = xr;
     } else if (fl) {   // long frame next to a short one: start / stop window
+        const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+        const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), bs_long_win(T, fl, i)); }, T, bufA, tid);
         if (st) XR = grp_mdct<256>([&](int i) { return __dmul_rn(rR(i), bs_long_win(T, fl, i)); }, T, bufB, tid);
     } else if (st) {   // both channels' MDCTs stage by stage together
+        const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+        const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
         if (!rL.f) {
             grp_mdct2<256>([&](int i, int u) { return __dmul_rn(stereo_sample(rL, i, u), T->sine[i]); },
                            T, bufA, bufB, tid);
@@ -744,6 +818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         XL = reinterpret_cast<const double*>(bufA);
         XR = reinterpret_cast<const double*>(bufB);
     } else {
+        const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
         XL = grp_mdct<256>([&](int i) { return __dmul_rn(rL(i), T->sine[i]); }, T, bufA, tid);
     }
     // (every MDCT ended with a barrier: the upper halves are free)
@@ -768,12 +843,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     lds_sync();
-    double xl4[4], xr4[4];
     double mL = 0.0, mR = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        xl4[i] = XL[i * 256 + tid];
-        xr4[i] = st ? XR[i * 256 + tid] : 0.0;
+        if constexpr (!FAST) {
+            xl4[i] = XL[i * 256 + tid];
+            xr4[i] = st ? XR[i * 256 + tid] : 0.0;
+        }
         mL = fmax(mL, fabs(xl4[i]));
         mR = fmax(mR, fabs(xr4[i]));
     }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Phase clocks of k_master_thr (PAC_DEBUG_FLAGS=128) at the bench geometry:
+# marks 0 start, 1 variant spectrum, 2 maskers + lists + scans, 3 rows (wave
+# end), 4 after the barrier, 5-7 the second variant, 8 end
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+PAC_DEBUG_FLAGS=128 timeout -k 10 120 python bench.py --no-cpu --config 2 --steps 1 --warmup 1 > gpurun_out/pt_thr.json 2> gpurun_out/pt_thr.err || exit 1
+grep -A9 PAC_PROF gpurun_out/pt_thr.err | tail -10

@@ -186,17 +186,22 @@ KERNEL_IO_BYTES = {
 }
 
 
-def master_launches(nb, chunk_blocks=65536):
+def master_launches(nb, chunk_blocks=32768):
     """launches of each pass-1 master kernel per pac_encode_streams call of
     streams with nb[i] blocks: one per chunk (run_master in pac_abi.hip:
-    groups of <= chunk_blocks streams, S = min(chunk_blocks / n_s, longest
-    stream) blocks per stream per chunk)"""
+    groups of <= chunk_blocks streams ordered by length, longest first; chunk
+    = S blocks of every stream still running at t0, S = min(chunk_blocks /
+    running streams, blocks left of the longest))"""
     n = 0
     for g0 in range(0, len(nb), chunk_blocks):
-        grp = nb[g0:g0 + chunk_blocks]
-        gmax = max(1, max(grp))
-        S = max(1, min(chunk_blocks // len(grp), gmax))
-        n += (gmax + S - 1) // S
+        grp = sorted(nb[g0:g0 + chunk_blocks], reverse=True)
+        gmax = max(1, grp[0])
+        n_act, t0 = len(grp), 0
+        while t0 < gmax:
+            while n_act > 1 and grp[n_act - 1] <= t0:
+                n_act -= 1
+            t0 += max(1, min(chunk_blocks // n_act, gmax - t0))
+            n += 1
     return n
 
 

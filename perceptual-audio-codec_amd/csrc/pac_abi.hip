@@ -358,6 +358,7 @@ struct pac_ctx {
     int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
     bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
     bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
+    bool side_early = false;               // PAC_SIDE_EARLY=1: side(i+2) beside thr(i+1), spectra double-buffered
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -374,7 +375,7 @@ struct pac_ctx {
     DevBuf<PacWavInfo> wav_info;
     DevBuf<int16_t> dec_pcm;
     DevBuf<double> dec_fpcm;
-    int64_t chunk_blocks = 65536;
+    int64_t chunk_blocks = 0;              // blocks per pass-1 chunk; 0: run_master's default
     int dbg = 0;                           // PAC_DEBUG_FLAGS (diagnostic builds of the timing only)
     // timing
     bool timing = false;
@@ -403,6 +404,8 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
     if (const char* f = getenv("PAC_FRONT_FAST")) c->front_fast = atoi(f) != 0;
+    if (const char* f = getenv("PAC_SIDE_EARLY")) c->side_early = atoi(f) != 0;
+    if (const char* f = getenv("PAC_CHUNK_BLOCKS")) c->chunk_blocks = atoll(f);
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
     const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -823,7 +826,10 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     const int nch = src.n_ch;                          // 2, or 1 (mono master extension)
     const int64_t G = nch * nblocks;
     const int nvar = nch == 2 ? 6 : 1;                 // threshold variants per block
-    const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : 1;
+    // blocks per chunk: PAC_CHUNK_BLOCKS / pac_set_chunk_blocks, else 32768 (65536 with
+    // block switching) -- measured: configs[2] 6.88 -> 6.97 M blocks/s and configs[3]
+    // 6.27 -> 6.59 M against 65536; configs[4] 5.39 M at 65536 against 5.30 M
+    const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : p->block_switch ? 65536 : 32768;
     // chunk geometry: groups [g0, g1) of at most CB streams, each ordered by
     // length (longest first, perm); chunk = blocks t0 .. t0+S-1 of the
     // group's streams still running at t0 (a prefix of that order), S =
@@ -856,7 +862,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure(cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure((c->side_early ? 2 : 1) * cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(3 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(3 * cbmax * 2 * PAC_NB)))
         return rc;
     pack = pack || dbg_codes;
@@ -895,8 +901,11 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     }
     // the MDCT lines from the side kernel's LRMS spectra (mdct_from_dft): sine
     // window, stereo, no block switching; otherwise the front transforms
-    const bool front_fast = c->front_fast && nch == 2 && !F.bsf && p->window == PAC_WINDOW_SINE && c->side_fused;
-    if (front_fast && (rc = c->m_mdct.ensure(2 * cbmax * 2 * PAC_HALFN))) return rc;
+    // (with block switching the plain long frames' lines; k_master_front<false>
+    // transforms the others)
+    const bool side_mdct = c->front_fast && nch == 2 && p->window == PAC_WINDOW_SINE && c->side_fused;
+    const bool front_fast = side_mdct && !F.bsf;
+    if (side_mdct && (rc = c->m_mdct.ensure(2 * cbmax * 2 * PAC_HALFN))) return rc;
     if (dbg_codes) {
         if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
             (rc = c->dbg_len.ensure(G * PAC_HALFN)))
@@ -950,8 +959,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         const int64_t k = i % 3;
         return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
-                                 c->m_spec.p, c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
-                                 front_fast ? c->m_mdct.p + (i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
+                                 c->m_spec.p + (c->side_early ? (i & 1) * cbmax * 2 * PAC_SPEC_LD : 0),
+                                 c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
+                                 side_mdct ? c->m_mdct.p + (i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
     };
     // PAC_DEBUG_FLAGS 32: phase clocks of the fused LRMS + spectra kernel, 64: of the front
     // 128: of the thresholds
@@ -982,12 +992,19 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         if ((rc2 = mark(2, 7))) return rc2;
         return PAC_OK;
     };
-    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr);
+    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr), spec_ev(nck + 1, nullptr);
+    const bool early = c->side_early && !serial;
     if ((rc = launch_side(0))) return rc;
     hipEvent_t spec_ready = event_on(s2);
+    spec_ev[0] = spec_ready;
+    if (early && nck > 1) {       // side(i+1) runs beside thr(i): spectra and MDCT lines double-buffered
+        if ((rc = launch_side(1))) return rc;
+        spec_ev[1] = event_on(s2);
+    }
     for (int64_t i = 0; i < nck; ++i) {
         const Chunk& q = chunks[i];
         const PacMasterChunkBuf K = bufset(i);
+        if (early) spec_ready = spec_ev[i];
         HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
         if (i >= 3) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
         if ((rc = mark(0, -1))) return rc;
@@ -1000,7 +1017,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             if ((rc = mark(0, 6))) return rc;
         }
         const hipEvent_t thr_done = event_on(s0);
-        if (i + 1 < nck) {                            // the next chunk's LRMS + spectra, beside this front
+        if (!early && i + 1 < nck) {                  // the next chunk's LRMS + spectra, beside this front
             HIPCHK(hipStreamWaitEvent(s2, thr_done, 0));
             if ((rc = launch_side(i + 1))) return rc;
             spec_ready = event_on(s2);
@@ -1012,10 +1029,16 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             hipLaunchKernelGGL(k_master_front<false>, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
         HIPCHK(hipGetLastError());
         if ((rc = mark(0, 1))) return rc;
+        const hipEvent_t front_done = event_on(s0);
+        if (early && i + 2 < nck) {                   // buffer set i & 1 is free once front(i) is done
+            HIPCHK(hipStreamWaitEvent(s2, front_done, 0));
+            if ((rc = launch_side(i + 2))) return rc;
+            spec_ev[i + 2] = event_on(s2);
+        }
         // the tail of this chunk once the next chunk's spectra are ready too,
         // i.e. beside the next chunk's thresholds
-        HIPCHK(hipStreamWaitEvent(s1, event_on(s0), 0));
-        if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, spec_ready, 0));
+        HIPCHK(hipStreamWaitEvent(s1, front_done, 0));
+        if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, early ? spec_ev[i + 1] : spec_ready, 0));
         if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
         if ((rc = mark(1, -1))) return rc;
         // few streams: a wave per stream (the one-lane chain's latency would

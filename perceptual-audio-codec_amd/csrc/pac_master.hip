@@ -719,8 +719,12 @@ __global__ __launch_bounds__(256) void k_master_lrms_spec(PacSource src, const P
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    // K.mdct: set by the host only for sine-window stereo calls without block switching
-    if (ck.nch == 2) lrms_block(src, T, F, cp, bufA, bufB, K.mdct ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
+    // K.mdct: set by the host only for sine-window stereo calls; the plain long
+    // frames' lines (block switching: the other frames transform in the front)
+    if (ck.nch == 2) {
+        const bool md = K.mdct && !(F.bsf && F.bsf[cp.gb]);
+        lrms_block(src, T, F, cp, bufA, bufB, md ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
+    }
     lds_sync();                                   // the leaf sums are read before the spectra overwrite them
     spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
 }
@@ -780,7 +784,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
     double xl4[4], xr4[4];
-    if constexpr (FAST) {
+    // the lines come from the side kernel (K.mdct): every block of a FAST call;
+    // with block switching, the plain long frames
+    const bool from_md = FAST || (K.mdct && st && !fl);
+    if (from_md) {
         const double* md = K.mdct + j * 2 * PAC_HALFN;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -790,10 +797,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
     const double* XL = nullptr;
     const double* XR = nullptr;
-    if constexpr (FAST) {
-    } else if (sh) {
+    if (from_md) {
+    } else if (sh) {   // four short MDCTs per channel, interleaved (scratch: the buffers' upper halves)
         const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
-        const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));          // four short MDCTs per channel, interleaved (scratch: the buffers' upper halves)
+        const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, st ? 1 : 0));
         double* xl = reinterpret_cast<double*>(bufA);
         double* xr = reinterpret_cast<double*>(bufB);
         grp_short_mdct(rL, T, bufA + 512, bufB + 512, xl, tid);
@@ -846,7 +853,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     double mL = 0.0, mR = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        if constexpr (!FAST) {
+        if (!from_md) {
             xl4[i] = XL[i * 256 + tid];
             xr4[i] = st ? XR[i * 256 + tid] : 0.0;
         }
@@ -1182,7 +1189,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 // --- the reservoir tail for few streams: one wave per stream --------------
 // The one-lane tail spends ~0.7 ms per block of a stream (its chain is a
 // string of dependent memory round trips), so a call with few streams --
-// S = 65536 / streams blocks per stream and chunk -- is bound by it.  For a
+// S = 32768 / streams blocks per stream and chunk -- is bound by it.  For a
 // chunk of at most PAC_WIDE_MAX streams this kernel runs the same chain with
 // a whole wave per stream: the 25 bands in lanes 0-24 (BitAlloc's argmax as a
 // DPP + permlane reduction), 16 lines per lane for the mantissas and the

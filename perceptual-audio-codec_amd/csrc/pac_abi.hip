@@ -359,6 +359,7 @@ struct pac_ctx {
     bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
     bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
     bool side_early = false;               // PAC_SIDE_EARLY=1: side(i+2) beside thr(i+1), spectra double-buffered
+    bool tail_early = false;               // PAC_TAIL_EARLY=1: tail(i) right after front(i) (A/B switch)
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -405,6 +406,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
     if (const char* f = getenv("PAC_FRONT_FAST")) c->front_fast = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_EARLY")) c->side_early = atoi(f) != 0;
+    if (const char* f = getenv("PAC_TAIL_EARLY")) c->tail_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_CHUNK_BLOCKS")) c->chunk_blocks = atoll(f);
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
@@ -1038,7 +1040,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         // the tail of this chunk once the next chunk's spectra are ready too,
         // i.e. beside the next chunk's thresholds
         HIPCHK(hipStreamWaitEvent(s1, front_done, 0));
-        if (i + 1 < nck) HIPCHK(hipStreamWaitEvent(s1, early ? spec_ev[i + 1] : spec_ready, 0));
+        if (i + 1 < nck && !c->tail_early) HIPCHK(hipStreamWaitEvent(s1, early ? spec_ev[i + 1] : spec_ready, 0));
         if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
         if ((rc = mark(1, -1))) return rc;
         // few streams: a wave per stream (the one-lane chain's latency would

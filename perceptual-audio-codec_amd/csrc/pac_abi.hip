@@ -148,6 +148,11 @@ static void build_tables(int fs, int window, PacTables* t) {
         double c = -2.0 * M_PI * k / 1024.0;
         t->fft_tw[k] = make_double2(cos(c), sin(c));
     }
+    static_assert(offsetof(PacTables, fft_tw4) == offsetof(PacTables, fft_tw) + PAC_HALFN * sizeof(double2),
+                  "tw4_of addresses the stage table from fft_tw");
+    for (int Ns = 4, b = 0; Ns <= 256; b += Ns, Ns *= 4)
+        for (int k = 0; k < Ns; k++)
+            for (int r = 1; r <= 3; r++) t->fft_tw4[3 * (b + k) + r - 1] = t->fft_tw[r * k * (256 / Ns)];
     for (int k = 0; k < PAC_HALFN; k++) {
         double a = -2.0 * M_PI * k / 2048.0;
         t->rfft_tw[k] = make_double2(cos(a), sin(a));

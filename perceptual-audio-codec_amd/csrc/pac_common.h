@@ -24,6 +24,10 @@ struct PacTables {
     // (cos a, sin a, cos b, sin b) / N, a, b = 2 pi n0 (k + 1/2)/N -+ pi/(2N)
     double4 mdct_tw2[PAC_HALFN];
     double2 fft_tw[PAC_HALFN];         // exp(-2 pi i k / 1024), k < 1024
+    // the radix-4 Stockham stages' twiddles W^e, W^2e, W^3e (e = k 256/Ns, k < Ns)
+    // stage-major, stage Ns = 4^s at [3 ((Ns - 4)/3 + k)] (tw4_of): right after
+    // fft_tw, so a kernel reaches them from the same pointer
+    double2 fft_tw4[3 * (4 + 16 + 64 + 256)];
     double2 rfft_tw[PAC_HALFN];        // exp(-2 pi i k / 2048), k < 1024
     double bark_line[PAC_HALFN];  // Bark(MDCTFreqs)                psychoac.py:434,95
     double tiq[PAC_HALFN];        // Intensity(Thresh(MDCTFreqs))   psychoac.py:437

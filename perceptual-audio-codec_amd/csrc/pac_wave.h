@@ -142,6 +142,14 @@ __device__ __forceinline__ void grp_fft(double2* buf, const double2* __restrict_
 // layout, so callers never see it.  Linear: fft_swz(a + b) =
 // fft_swz(a) ^ fft_swz(b) for bit-disjoint a, b (one swizzle per butterfly,
 // the other offsets are compile-time constants).
+// the twiddles W^e, W^2e, W^3e (e = k 256/Ns) of a radix-4 stage Ns >= 4 from the
+// stage-major table after fft_tw (PacTables::fft_tw4): one contiguous run per
+// wave instead of three strided reads of fft_tw (3x fewer cache lines in the
+// late stages); the same values, bit-identical
+__device__ __forceinline__ const double2* tw4_of(const double2* __restrict__ tw, int Ns, int k) {
+    return tw + PAC_HALFN + 3 * ((Ns - 4) / 3 + k);
+}
+
 __host__ __device__ constexpr int fft_swz(int i) {
     return (((i >> 3) & 1) * 1) ^ (((i >> 4) & 1) * 14) ^ (((i >> 5) & 1) * 2) ^ (((i >> 6) & 1) * 1) ^
            (((i >> 7) & 1) * 7);
@@ -171,11 +179,11 @@ __device__ __forceinline__ double2* grp_fft_stockham(double2* src, double2* dst,
             double2 v0 = src[j ^ xj], v1 = src[(j + N4) ^ xj ^ (swi ? fft_swz(N4) : 0)];
             double2 v2 = src[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
             double2 v3 = src[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
-            if (Ns > 1) {
-                const int e = k * (256 / Ns);           // angle -2 pi k r / (4 Ns)
-                v1 = cmul(v1, tw[e]);
-                v2 = cmul(v2, tw[2 * e]);
-                v3 = cmul(v3, tw[3 * e]);
+            if (Ns > 1) {                               // angles -2 pi k r / (4 Ns)
+                const double2* w = tw4_of(tw, Ns, k);
+                v1 = cmul(v1, w[0]);
+                v2 = cmul(v2, w[1]);
+                v3 = cmul(v3, w[2]);
             }
             const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
             const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
@@ -235,10 +243,10 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
             v[q][2] = buf[(j + 2 * N4) ^ xj ^ (swi ? fft_swz(2 * N4) : 0)];
             v[q][3] = buf[(j + 3 * N4) ^ xj ^ (swi ? fft_swz(3 * N4) : 0)];
             if (Ns > 1) {
-                const int e = k * (256 / Ns);
-                v[q][1] = cmul(v[q][1], tw[e]);
-                v[q][2] = cmul(v[q][2], tw[2 * e]);
-                v[q][3] = cmul(v[q][3], tw[3 * e]);
+                const double2* w = tw4_of(tw, Ns, k);
+                v[q][1] = cmul(v[q][1], w[0]);
+                v[q][2] = cmul(v[q][2], w[1]);
+                v[q][3] = cmul(v[q][3], w[2]);
             }
         }
         grp_sync<NT>();
@@ -325,10 +333,10 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
                     v[u][q][1] = bufs[u][(j + N4) ^ xj ^ fft_swz(N4)];
                     v[u][q][2] = bufs[u][(j + 2 * N4) ^ xj ^ fft_swz(2 * N4)];
                     v[u][q][3] = bufs[u][(j + 3 * N4) ^ xj ^ fft_swz(3 * N4)];
-                    const int e = k * (256 / Ns);
-                    v[u][q][1] = cmul(v[u][q][1], tw[e]);
-                    v[u][q][2] = cmul(v[u][q][2], tw[2 * e]);
-                    v[u][q][3] = cmul(v[u][q][3], tw[3 * e]);
+                    const double2* w = tw4_of(tw, Ns, k);
+                    v[u][q][1] = cmul(v[u][q][1], w[0]);
+                    v[u][q][2] = cmul(v[u][q][2], w[1]);
+                    v[u][q][3] = cmul(v[u][q][3], w[2]);
                 }
             grp_sync<NT>();
         }
@@ -391,10 +399,10 @@ __device__ __forceinline__ void grp_fft_stockham_x2_ld(double2* sa, double2* da,
             v1 = src[(j + N4) ^ xj ^ fft_swz(N4)];
             v2 = src[(j + 2 * N4) ^ xj ^ fft_swz(2 * N4)];
             v3 = src[(j + 3 * N4) ^ xj ^ fft_swz(3 * N4)];
-            const int e = k * (256 / Ns);
-            v1 = cmul(v1, tw[e]);
-            v2 = cmul(v2, tw[2 * e]);
-            v3 = cmul(v3, tw[3 * e]);
+            const double2* w = tw4_of(tw, Ns, k);
+            v1 = cmul(v1, w[0]);
+            v2 = cmul(v2, w[1]);
+            v3 = cmul(v3, w[2]);
         }
         const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
         const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);

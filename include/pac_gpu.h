@@ -253,6 +253,10 @@ int pac_debug_threshold(pac_ctx *ctx, int32_t sample_rate, int32_t n, const doub
 /* Parity probe: SineWindow + MDCT (window.py:27-39, mdct.py:49-82) of n raw
  * 2048-sample blocks -> 1024 lines each (before the overall scale). */
 int pac_debug_mdct(pac_ctx *ctx, int32_t n, const double *data, double *X);
+/* Parity probe of the master path's MDCT: the same lines derived from the raw
+ * blocks' DFT as k_master_lrms_spec derives them from the LRMS spectra
+ * (mdct_from_dft; blocks taken in pairs as the L and R of one stereo block). */
+int pac_debug_mdct_dft(pac_ctx *ctx, int32_t n, const double *data, double *X);
 
 #ifdef __cplusplus
 }

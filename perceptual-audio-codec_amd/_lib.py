@@ -131,6 +131,7 @@ def lib():
         "pac_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "pac_debug_threshold": (C.c_int, [vp, i32, i32, vp, i32, vp, vp]),
         "pac_debug_mdct": (C.c_int, [vp, i32, vp, vp]),
+        "pac_debug_mdct_dft": (C.c_int, [vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -371,6 +372,12 @@ class Context:
         d = np.ascontiguousarray(np.atleast_2d(data), dtype=np.float64)
         X = np.zeros((d.shape[0], 1024))
         check(self.L.pac_debug_mdct(self.h, d.shape[0], d.ctypes.data, X.ctypes.data))
+        return X
+
+    def debug_mdct_dft(self, data):
+        d = np.ascontiguousarray(np.atleast_2d(data), dtype=np.float64)
+        X = np.zeros((d.shape[0], 1024))
+        check(self.L.pac_debug_mdct_dft(self.h, d.shape[0], d.ctypes.data, X.ctypes.data))
         return X
 
     def sync(self):

@@ -1466,6 +1466,24 @@ extern "C" int pac_debug_mdct(pac_ctx* c, int32_t n, const double* data, double*
     return PAC_OK;
 }
 
+extern "C" int pac_debug_mdct_dft(pac_ctx* c, int32_t n, const double* data, double* X) {
+    if (!c || !data || !X || n < 1) return set_err(PAC_E_ARG, "bad argument");
+    int rc;
+    HIPCHK(hipSetDevice(c->device));
+    PacTables* T;
+    if ((rc = get_tables(c, 48000, PAC_WINDOW_SINE, &T))) return rc;
+    double *dd = nullptr, *dx = nullptr;
+    HIPCHK(hipMalloc((void**)&dd, (size_t)n * PAC_N * sizeof(double)));
+    HIPCHK(hipMalloc((void**)&dx, (size_t)n * PAC_HALFN * sizeof(double)));
+    HIPCHK(hipMemcpy(dd, data, (size_t)n * PAC_N * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_mdct_dft, dim3((unsigned)((n + 1) / 2)), dim3(256), 0, c->stream, T, dd, n, dx);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(X, dx, (size_t)n * PAC_HALFN * sizeof(double), hipMemcpyDeviceToHost));
+    hipFree(dd); hipFree(dx);
+    return PAC_OK;
+}
+
 extern "C" int pac_set_chunk_blocks(pac_ctx* c, int64_t blocks) {
     if (!c || blocks < 1) return set_err(PAC_E_ARG, "bad argument");
     c->chunk_blocks = blocks;

@@ -524,6 +524,36 @@ __device__ __forceinline__ double mdct_from_dft(double2 x0, double2 x1, const Pa
     return r == 0.0 ? (T->mdct_zero_neg[k] ? -0.0 : 0.0) : r;
 }
 
+// parity probe (pac_debug_mdct_dft): blocks 2 i, 2 i + 1 of `data` (n blocks
+// of 2048 raw samples) as the L and R of one block, the MDCT lines of both
+// exactly as lrms_block derives them (same FFT, same split, mdct_from_dft)
+__global__ __launch_bounds__(256) void k_debug_mdct_dft(const PacTables* __restrict__ T,
+                                                        const double* __restrict__ data, int n,
+                                                        double* __restrict__ X) {
+    __shared__ double2 bufA[1024], bufB[1024];
+    const int tid = threadIdx.x;
+    const int64_t b0 = 2 * (int64_t)blockIdx.x;
+    const double* dA = data + b0 * PAC_N;
+    const double* dB = b0 + 1 < n ? dA + PAC_N : nullptr;
+    double nyA = 0.0, nyB = 0.0;
+    grp_spectrum_cplx2p_put<256>([&](int q) {
+        return make_double4(dA[2 * q], dA[2 * q + 1], dB ? dB[2 * q] : 0.0, dB ? dB[2 * q + 1] : 0.0);
+    }, T, bufA, bufB, tid, [&](int u, int k, double2 Z) {
+        if (k < 1024) (u ? bufB : bufA)[k] = Z;
+        else if (u) nyB = Z.x;
+        else nyA = Z.x;
+    });
+    lds_sync();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = 1023 - 256 * i - tid;
+        const double2 a1 = k == 1023 ? make_double2(nyA, 0.0) : bufA[k + 1];
+        const double2 b1 = k == 1023 ? make_double2(nyB, 0.0) : bufB[k + 1];
+        X[b0 * PAC_HALFN + k] = mdct_from_dft(bufA[k], a1, T, k);
+        if (dB) X[(b0 + 1) * PAC_HALFN + k] = mdct_from_dft(bufB[k], b1, T, k);
+    }
+}
+
 __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables* __restrict__ T,
                                            const PacMasterFields& F, const ChunkPos& cp, double2* bufA,
                                            double2* bufB, double* __restrict__ mdct) {

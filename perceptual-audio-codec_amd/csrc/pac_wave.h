@@ -710,7 +710,8 @@ __device__ __forceinline__ int lsw(int m) { return m ^ (((m >> 5) & 3) << 1); }
 // without a source get the identity 0): inclusive prefix of a double, and of a
 // double-double (hi, lo) pair
 #define PAC_DPP_SHR(n) (0x110 + (n))
-#define PAC_DPP_WSHR1 0x138
+#define PAC_DPP_WSHR1 0x138     // wave_shr:1 (lane i <- lane i - 1)
+#define PAC_DPP_WSHL1 0x130     // wave_shl:1 (lane i <- lane i + 1)
 template <int CTRL, int RM = 0xf>
 __device__ __forceinline__ void scan_step(double& x) { x += dpp_f64<CTRL, RM>(0.0, x); }
 __device__ __forceinline__ double wave_incl_scan_f64(double x) {

@@ -66,3 +66,26 @@ def test_threshold_vs_oracle(ctx, fs, kind, no_drop):
         assert npk[i] == len(peaks)
         worst = max(worst, np.max(np.abs(thr[i] - ref)))
     assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("kind", ["white", "pink", "quiet", "loud"])
+def test_mdct_from_dft_vs_oracle(ctx, kind):
+    """The master path's MDCT lines (k_master_lrms_spec: from the raw block's DFT,
+    mdct_from_dft) against the oracle's restatement of mdct.py -- the same bar as
+    the front's DCT-IV (odd n: the last block is transformed alone)."""
+    x = blocks(kind, 33, 5)
+    X = ctx.debug_mdct_dft(x)
+    o = P.Oracle(48000, huffman=False)
+    worst = 0.0
+    for i in range(x.shape[0]):
+        ref = o.mdct(x[i] * np.sin((np.arange(2048) + 0.5) * np.pi / 2048))
+        err = np.max(np.abs(X[i] - ref)) / max(np.max(np.abs(ref)), 1e-300)
+        worst = max(worst, err)
+    assert worst < 1e-12, worst
+
+
+def test_mdct_from_dft_zero_signs(ctx):
+    X = ctx.debug_mdct_dft(np.zeros((2, 2048)))
+    Y = P.Oracle(48000, huffman=False).mdct(np.zeros(2048))
+    for i in range(2):
+        assert np.all(X[i] == 0) and np.array_equal(np.signbit(X[i]), np.signbit(Y))

@@ -165,12 +165,27 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
         for (int i = 0; i < 4; ++i) X[i] = P[i];
     } else {
         const double sg = (v & 1) ? -1.0 : 1.0;      // M = (a + b)/2, S = (a - b)/2
+        auto ms = [&](int o) {                       // bin k0 + o - 2 of M or S
+            const double2 a = S[k0 + o], b = S[PAC_SPEC_LD + k0 + o];
+            return make_double2(0.5 * (a.x + sg * b.x), 0.5 * (a.y + sg * b.y));
+        };
         double2 m[8];                                // bins k0 - 2 .. k0 + 5
+        // the thread's own four bins from memory, the two on each side from the
+        // neighbouring lanes (DPP wave shifts; the same values): half the loads;
+        // a wave's edge lanes load theirs
+        const int lane = tid & (WAVE - 1);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const double2 a = S[k0 + i], b = S[PAC_SPEC_LD + k0 + i];
-            m[i] = make_double2(0.5 * (a.x + sg * b.x), 0.5 * (a.y + sg * b.y));
-        }
+        for (int i = 2; i < 6; ++i) m[i] = ms(i);
+        auto sh = [](double2 x, auto ctrl) {
+            constexpr int C = decltype(ctrl)::value;
+            return make_double2(dpp_f64<C>(x.x, x.x), dpp_f64<C>(x.y, x.y));
+        };
+        m[0] = sh(m[4], std::integral_constant<int, PAC_DPP_WSHR1>{});
+        m[1] = sh(m[5], std::integral_constant<int, PAC_DPP_WSHR1>{});
+        m[6] = sh(m[2], std::integral_constant<int, PAC_DPP_WSHL1>{});
+        m[7] = sh(m[3], std::integral_constant<int, PAC_DPP_WSHL1>{});
+        if (lane == 0) { m[0] = ms(0); m[1] = ms(1); }
+        if (lane == WAVE - 1) { m[6] = ms(6); m[7] = ms(7); }
         double2 h[6];                                // M h at bins k0 - 1 .. k0 + 4
 #pragma unroll
         for (int i = 0; i < 6; ++i) h[i] = hann_tap(m[i], m[i + 1], m[i + 2]);

@@ -155,7 +155,7 @@ __device__ __forceinline__ double2 hann_tap(double2 xm, double2 x0, double2 xp) 
 // bank slots (the 4 consecutive doubles at a 32-byte lane stride would be a
 // 2-way conflict, the old double2 .x layout an 8-way one).
 template <int NT>
-__device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, int v, double2* buf, int tid) {
+__device__ __forceinline__ void grp_variant_pow_regs(const double2* __restrict__ S, int v, int tid, double (&p)[4]) {
     static_assert(NT * 4 == 1024, "4 bins per thread");
     const int k0 = 4 * tid;
     double2 X[4];
@@ -192,9 +192,12 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
 #pragma unroll
         for (int i = 0; i < 4; ++i) X[i] = v < 4 ? h[i + 1] : hann_tap(h[i], h[i + 1], h[i + 2]);
     }
-    double p[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) p[i] = __builtin_fma(X[i].x, X[i].x, X[i].y * X[i].y);
+}
+// ... stored to LDS (the thread's 4 bins as two 16-byte halves, see above)
+template <int NT>
+__device__ __forceinline__ void grp_variant_pow_store(const double (&p)[4], double2* buf, int tid) {
     double2* pw2 = reinterpret_cast<double2*>(buf);
     const bool sw = tid & 4;
     pw2[2 * tid + (sw ? 1 : 0)] = sw ? make_double2(p[2], p[3]) : make_double2(p[0], p[1]);
@@ -211,12 +214,12 @@ __device__ __forceinline__ void grp_variant_pow(const double2* __restrict__ S, i
         if (pm && (threadIdx.x & (WAVE - 1)) == 0)                                                   \
             pm[(threadIdx.x / WAVE) * PAC_PROF_MARKS + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
     } while (0)
-__device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double2* __restrict__ spec,
+// (p: the thread's four bins of the variant's |V[k]|^2, grp_variant_pow_regs)
+__device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double (&p)[4],
                                          double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
                                          int tid, long long* pm, int mk) {
     const int lane = tid & (WAVE - 1);
-    // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
-    grp_variant_pow<FRONT_NT>(spec, v, buf, tid);
+    grp_variant_pow_store<FRONT_NT>(p, buf, tid);
     TPROF(mk);
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(reinterpret_cast<const double*>(buf), T, v >= 4 ? 0.0 : 15.0, tid, L);
@@ -279,13 +282,19 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     long long* pm = (src.prof && blockIdx.x < PAC_PROF_WG) ? src.prof + (int64_t)blockIdx.x * 4 * PAC_PROF_MARKS
                                                           : nullptr;
     TPROF(0);
-    thr_variant(T, spec, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
+    // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
+    double p[4];
+    grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
+    thr_variant(T, p, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
     if (ck.nch != 2) return;
-    lds_sync();                                             // the first variant's lists are read
-    TPROF(4);
     int t2 = tid;                // opaque copy: no per-lane address of the first call is kept live for the second
     asm volatile("" : "+v"(t2));
-    thr_variant(T, spec, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2, pm, 5);
+    // the second variant's spectrum in registers while the other waves finish
+    // the first one's rows (no LDS touched), then stored after the barrier
+    grp_variant_pow_regs<FRONT_NT>(spec, vb + 1, t2, p);
+    lds_sync();                                             // the first variant's lists are read
+    TPROF(4);
+    thr_variant(T, p, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2, pm, 5);
     TPROF(8);
 }
 

@@ -888,8 +888,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // together (the selection loop below stores to HBM, which the compiler
     // cannot move these loads across): L, R or M, S and the MLD-scaled M, S
     const double* thr = K.thr + j * 6 * PAC_HALFN;
-    // (branch-free: an L/R line loads M/S-plane values it does not use, so no
-    // load waits inside a branch); the MLD pair arrives as MLD_M, MLD_S
+    // (the MLD pair under the line's mode mask: an L/R line fetches 16 B, an
+    // M/S line 32 B -- the front is HBM-heavy, 50 KB per block); the MLD pair arrives as MLD_M, MLD_S
     double t4[4][4];
     int ms4[4];
 #pragma unroll
@@ -899,8 +899,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const double* tp = thr + (ms4[i] ? 2 * PAC_HALFN : 0) + l;
         t4[i][0] = tp[0];
         t4[i][1] = tp[PAC_HALFN];
-        t4[i][2] = tp[2 * PAC_HALFN];
-        t4[i][3] = tp[3 * PAC_HALFN];
+        t4[i][2] = t4[i][3] = 0.0;
+        if (ms4[i]) {                  // the MLD pair: M/S lines only (masked lanes fetch nothing)
+            t4[i][2] = tp[2 * PAC_HALFN];
+            t4[i][3] = tp[3 * PAC_HALFN];
+        }
     }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     lds_sync();

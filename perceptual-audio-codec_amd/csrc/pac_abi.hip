@@ -415,10 +415,18 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_CHUNK_BLOCKS")) c->chunk_blocks = atoll(f);
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
-    const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess &&
-                    hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) == hipSuccess;
+    // PAC_STREAM_PRIO (experiment): four digits, one per stream (thr/front, tail,
+    // side, emit): 0 = the device's greatest priority, 1 = normal, 2 = least
+    int prio[4] = {1, 1, 1, 1};
+    if (const char* f = getenv("PAC_STREAM_PRIO"))
+        for (int k = 0; k < 4 && f[k]; ++k) prio[k] = std::min(2, std::max(0, f[k] - '0'));
+    int plo = 0, phi = 0;
+    if (hipDeviceGetStreamPriorityRange(&plo, &phi) != hipSuccess) plo = phi = 0;
+    auto mk_stream = [&](hipStream_t* s, int k) {
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, phi + (plo - phi) * prio[k] / 2) == hipSuccess;
+    };
+    const bool ok = mk_stream(&c->stream, 0) && mk_stream(&c->stream2, 1) && mk_stream(&c->stream3, 2) &&
+                    mk_stream(&c->stream4, 3);
     if (!ok) {
         delete c;
         return set_err(PAC_E_HIP, "hipStreamCreate failed");
@@ -1585,7 +1593,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
                        (long long)pcm_capacity_frames);
     if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
     const int64_t G1 = G > 0 ? G : 1;
-    if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(G1 * PAC_HALFN)) ||
+    if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(((G1 + 63) & ~63LL) * PAC_HALFN)) ||
         (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
         (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)) ||
         (p->block_switch && (rc = c->dec_bsf.ensure(G1))))

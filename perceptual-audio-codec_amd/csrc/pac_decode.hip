@@ -135,9 +135,20 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
     return sym == 0xffffu ? r.read(ba) : sym;   // escape: the raw ba-bit symbol follows
 }
 
-// Per-channel-block fields: codes [G][1024] (signed mantissa codes as the
-// reference's ReadDataBlock builds them), ba/sf [G][25], overall [G],
+// Per-channel-block fields: codes (signed mantissa codes as the reference's
+// ReadDataBlock builds them, layout dec_code_at), ba/sf [G][25], overall [G],
 // lrms [G][25] (master).
+//
+// The codes are tiled: tile (g / 64, l / 16) holds lines l .. l+15 of the 64
+// channel-blocks g of one parse wave as 64 runs of 16 codes (2 KB).  A parse
+// lane writes its lines in order, so a 128-byte line of the tile is complete
+// once four neighbouring lanes have passed 16 lines -- the plain [G][1024]
+// layout left every lane its own partly written line for 64 lines, more open
+// lines than the L2 holds (the parse wrote ~10x the codes' bytes to HBM);
+// the synthesis reads 32 contiguous bytes per 16 threads.
+__device__ __forceinline__ int64_t dec_code_at(int64_t g, int l) {
+    return (((g >> 6) * (PAC_HALFN / 16) + (l >> 4)) << 10) + ((g & 63) << 4) + (l & 15);
+}
 struct PacDecWork {
     uint16_t* codes;
     uint8_t* ba;
@@ -162,7 +173,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
     r.init(p + 4, 0, end);
     D.overall[g] = (uint8_t)r.read(4);
     const int id = master ? (int)r.read(4) - 1 : 0;
-    uint16_t* codes = D.codes + g * PAC_HALFN;
+    uint16_t* codes = D.codes + dec_code_at(g, 0);     // + dec_code_at(0, l): l's slot in g's tiles
     int64_t bit = master ? 8 : 4;         // bit position, for the sign-bit reader
     for (int b = 0; b < PAC_NB; ++b) {
         int a = (int)r.read(4);
@@ -173,7 +184,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
         if (!a) continue;
         const int lo = T->lower[b], nl = T->nlines[b];
         if (!master) {
-            for (int l = lo; l < lo + nl; ++l) codes[l] = (uint16_t)r.read(a);
+            for (int l = lo; l < lo + nl; ++l) codes[dec_code_at(0, l)] = (uint16_t)r.read(a);
             bit += (int64_t)nl * a;
         } else {
             DecBits sg;                            // nl sign bits, then nl Huffman codes
@@ -183,7 +194,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
             const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
             for (int l = lo; l < lo + nl; ++l) {
                 const uint32_t sym = dec_huff(r, htab, hd, tid, a);
-                codes[l] = (uint16_t)(sym + (sg.read(1) << (a - 1)));
+                codes[dec_code_at(0, l)] = (uint16_t)(sym + (sg.read(1) << (a - 1)));
             }
             bit = -1;                              // recomputed below from the main reader
         }
@@ -229,7 +240,7 @@ __device__ __forceinline__ void grp_dequant(const PacTables* __restrict__ T, con
         const int b = T->band_of_line[l];
         const int ba = (l < T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1]) ? D.ba[g * PAC_NB + b] : 0;
         double v = 0.0;
-        if (ba) v = pac_dequantize(D.sf[g * PAC_NB + b], D.codes[g * PAC_HALFN + l], ba);
+        if (ba) v = pac_dequantize(D.sf[g * PAC_NB + b], D.codes[dec_code_at(g, l)], ba);
         L[l] = v / rescale;
     }
 }

@@ -620,6 +620,19 @@ extern "C" int pac_huffman_load(pac_ctx* c, const uint8_t* buf, int64_t len) {
         c->hdec.maxlen[t] = ml;
         c->hdec.l1[t] = l1;
     }
+    // the short-code table (PacHuffDec.sbase): every code of at most
+    // PAC_DEC_SBITS bits over all its PAC_DEC_SBITS-bit extensions
+    c->hdec.sbase = (int32_t)tab.size();
+    tab.resize(tab.size() + ((size_t)PAC_NTAB << PAC_DEC_SBITS), 0x80000000u);
+    for (int t = 0; t < PAC_NTAB; t++)
+        for (int sym = -1; sym < PAC_NSYM; sym++) {
+            const int len = sym < 0 ? h->esc_len[t] : h->len[t][sym];
+            if (!len || len > PAC_DEC_SBITS) continue;
+            const uint32_t code = sym < 0 ? h->esc_bits[t] : h->bits[t][sym];
+            const uint32_t ent = ((uint32_t)len << 16) | (sym < 0 ? 0xffffu : (uint32_t)sym);
+            const uint32_t first = code << (PAC_DEC_SBITS - len), n = 1u << (PAC_DEC_SBITS - len);
+            for (uint32_t i = 0; i < n; i++) tab[c->hdec.sbase + ((size_t)t << PAC_DEC_SBITS) + first + i] = ent;
+        }
     free(h);
     if ((rc2 = c->hdec_tab.ensure(tab.size()))) return rc2;
     HIPCHK(hipMemcpy(c->hdec_tab.p, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));

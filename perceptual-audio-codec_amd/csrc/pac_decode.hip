@@ -25,10 +25,17 @@
 // level 1 indexed by the first l1 bits of the next maxlen bits; an entry is
 // (len << 16) | symbol, symbol 0xFFFF = the escape code, or 0x80000000 | the
 // offset of a level-2 table indexed by the remaining maxlen - l1 bits.
+// Plus the short-code table at sbase: PAC_NTAB x 2^PAC_DEC_SBITS entries
+// indexed by the next PAC_DEC_SBITS bits, (len << 16) | symbol for codes of at
+// most that length, 0x80000000 for the longer ones (then the two-level
+// lookup).  k_dec_parse holds it in LDS: 93-99 % of the symbols (the tables'
+// own code-length mass) decode without a global gather.
+#define PAC_DEC_SBITS 9
 struct PacHuffDec {
     int32_t base[PAC_NTAB];
     int32_t maxlen[PAC_NTAB];
     int32_t l1[PAC_NTAB];
+    int32_t sbase;
 };
 
 #define DEC_SEG 16      // blocks per synthesis workgroup
@@ -123,11 +130,15 @@ __device__ __forceinline__ int64_t bits_consumed(const DecBits& r, const uint8_t
 }
 
 __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restrict__ tab, const PacHuffDec& hd,
-                                             int id, int ba) {
-    const int ml = hd.maxlen[id], l1 = hd.l1[id];
-    const uint32_t idx = r.peek32() >> (32 - ml);
-    uint32_t e = tab[hd.base[id] + (idx >> (ml - l1))];
-    if (e >> 31) e = tab[(e & 0x7fffffffu) + (idx & ((1u << (ml - l1)) - 1u))];
+                                             const uint32_t* stab, int id, int ba) {
+    const uint32_t top = r.peek32();
+    uint32_t e = stab[(id << PAC_DEC_SBITS) + (top >> (32 - PAC_DEC_SBITS))];
+    if (e >> 31) {                           // a longer code: the two-level tables
+        const int ml = hd.maxlen[id], l1 = hd.l1[id];
+        const uint32_t idx = top >> (32 - ml);
+        e = tab[hd.base[id] + (idx >> (ml - l1))];
+        if (e >> 31) e = tab[(e & 0x7fffffffu) + (idx & ((1u << (ml - l1)) - 1u))];
+    }
     int len = (e >> 16) & 31;
     uint32_t sym = e & 0xffffu;
     if (!len) { len = 1; sym = 0; }         // not a code of the table: malformed input
@@ -164,6 +175,11 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
                                                    const PacTables* __restrict__ T,
                                                    const uint32_t* __restrict__ htab, PacHuffDec hd,
                                                    PacDecWork D) {
+    __shared__ uint32_t stab[PAC_NTAB << PAC_DEC_SBITS];   // 20 KB: 8 workgroups per CU
+    if (master) {
+        for (int i = threadIdx.x; i < (PAC_NTAB << PAC_DEC_SBITS); i += blockDim.x) stab[i] = htab[hd.sbase + i];
+        __syncthreads();
+    }
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint8_t* p = data + cb_off[g];
@@ -193,7 +209,7 @@ __global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ d
             bit += nl;
             const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
             for (int l = lo; l < lo + nl; ++l) {
-                const uint32_t sym = dec_huff(r, htab, hd, tid, a);
+                const uint32_t sym = dec_huff(r, htab, hd, stab, tid, a);
                 codes[dec_code_at(0, l)] = (uint16_t)(sym + (sg.read(1) << (a - 1)));
             }
             bit = -1;                              // recomputed below from the main reader

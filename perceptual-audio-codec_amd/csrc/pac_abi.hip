@@ -1606,7 +1606,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
                        (long long)pcm_capacity_frames);
     if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
     const int64_t G1 = G > 0 ? G : 1;
-    if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(((G1 + 63) & ~63LL) * PAC_HALFN)) ||
+    if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(((G1 + DEC_PARSE_NT - 1) / DEC_PARSE_NT) * DEC_PARSE_NT * PAC_HALFN)) ||
         (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
         (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)) ||
         (p->block_switch && (rc = c->dec_bsf.ensure(G1))))
@@ -1640,7 +1640,8 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
                            c->dec_cbbase.p, c->dec_cboff.p);
         PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p, c->dec_err.p,
                      p->block_switch ? c->dec_bsf.p : nullptr};
-        hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, ddev, c->dec_cboff.p, G,
+        hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + DEC_PARSE_NT - 1) / DEC_PARSE_NT)), dim3(DEC_PARSE_NT), 0, s,
+                           ddev, c->dec_cboff.p, G,
                            (int)master, T, master ? c->hdec_tab.p : nullptr, c->hdec, D);
         HIPCHK(hipGetLastError());
         if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));

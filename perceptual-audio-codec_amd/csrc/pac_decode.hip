@@ -150,15 +150,18 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
 // ReadDataBlock builds them, layout dec_code_at), ba/sf [G][25], overall [G],
 // lrms [G][25] (master).
 //
-// The codes are tiled: tile (g / 64, l / 16) holds lines l .. l+15 of the 64
-// channel-blocks g of one parse wave as 64 runs of 16 codes (2 KB).  A parse
-// lane writes its lines in order, so a 128-byte line of the tile is complete
-// once four neighbouring lanes have passed 16 lines -- the plain [G][1024]
-// layout left every lane its own partly written line for 64 lines, more open
-// lines than the L2 holds (the parse wrote ~10x the codes' bytes to HBM);
-// the synthesis reads 32 contiguous bytes per 16 threads.
+// The codes are tiled: tile (g / 64, l / 8) holds lines l .. l+7 of the 64
+// channel-blocks g of one parse wave as 64 runs of 8 codes (1 KB).  The parse
+// stages each lane's codes of the current 8-line group in LDS and writes the
+// group as one 16-byte store per lane -- 1 KB contiguous per wave, every
+// cache line whole at once.  (The plain [G][1024] layout, one 2-byte store per
+// line, left every lane its own partly written line open for 64 lines, more
+// open lines than the L2 holds: the parse wrote 41.4 KB to HBM per block for
+// 4 KB of codes.)  The synthesis reads 16 contiguous bytes per 8 threads.
+#define DEC_GRP 8
 __device__ __forceinline__ int64_t dec_code_at(int64_t g, int l) {
-    return (((g >> 6) * (PAC_HALFN / 16) + (l >> 4)) << 10) + ((g & 63) << 4) + (l & 15);
+    return (((g >> 6) * (PAC_HALFN / DEC_GRP) + (l / DEC_GRP)) * (WAVE * DEC_GRP)) + ((g & 63) * DEC_GRP) +
+           (l % DEC_GRP);
 }
 struct PacDecWork {
     uint16_t* codes;
@@ -170,56 +173,88 @@ struct PacDecWork {
     uint8_t* bsf;       // [G] block switching (pac_bs.h): the short-frame bit, or null: off
 };
 
-__global__ __launch_bounds__(256) void k_dec_parse(const uint8_t* __restrict__ data,
-                                                   const int64_t* __restrict__ cb_off, int64_t G, int master,
-                                                   const PacTables* __restrict__ T,
-                                                   const uint32_t* __restrict__ htab, PacHuffDec hd,
-                                                   PacDecWork D) {
-    __shared__ uint32_t stab[PAC_NTAB << PAC_DEC_SBITS];   // 20 KB: 8 workgroups per CU
+#define DEC_PARSE_NT 512
+__global__ __launch_bounds__(DEC_PARSE_NT) void k_dec_parse(const uint8_t* __restrict__ data,
+                                                            const int64_t* __restrict__ cb_off, int64_t G, int master,
+                                                            const PacTables* __restrict__ T,
+                                                            const uint32_t* __restrict__ htab, PacHuffDec hd,
+                                                            PacDecWork D) {
+    __shared__ uint32_t stab[PAC_NTAB << PAC_DEC_SBITS];   // 20 KB
+    // each lane's codes of the current DEC_GRP-line group (8 KB: 28 KB per
+    // workgroup of 8 waves, 4 workgroups = 8 waves per SIMD)
+    __shared__ __attribute__((aligned(16))) uint16_t stage[DEC_PARSE_NT][DEC_GRP];
     if (master) {
         for (int i = threadIdx.x; i < (PAC_NTAB << PAC_DEC_SBITS); i += blockDim.x) stab[i] = htab[hd.sbase + i];
         __syncthreads();
     }
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G) return;
-    const uint8_t* p = data + cb_off[g];
-    const uint32_t nbytes = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
-    const uint8_t* end = p + 4 + nbytes;
+    // lanes past G stay in the (wave-uniform) line loops with an empty reader
+    // (zero bits: every band unallocated) and store nothing but their staged
+    // codes, into the tile padding (the buffer holds whole waves)
+    const bool valid = g < G;
+    const uint8_t* p = data + (valid ? cb_off[g] : 0);
+    const uint32_t nbytes = valid ? (p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)) : 0u;
+    const uint8_t* end = valid ? p + 4 + nbytes : p;
     DecBits r;
     r.init(p + 4, 0, end);
-    D.overall[g] = (uint8_t)r.read(4);
+    const uint32_t ov = r.read(4);
+    if (valid) D.overall[g] = (uint8_t)ov;
     const int id = master ? (int)r.read(4) - 1 : 0;
-    uint16_t* codes = D.codes + dec_code_at(g, 0);     // + dec_code_at(0, l): l's slot in g's tiles
+    const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
+    uint16_t* st = stage[threadIdx.x];
+    int gcur = -1;                        // the staged group (wave-uniform)
+    auto flush = [&]() {
+        if (gcur >= 0)
+            *reinterpret_cast<uint4*>(D.codes + dec_code_at(g, gcur * DEC_GRP)) = *reinterpret_cast<const uint4*>(st);
+    };
     int64_t bit = master ? 8 : 4;         // bit position, for the sign-bit reader
     for (int b = 0; b < PAC_NB; ++b) {
         int a = (int)r.read(4);
         if (a) a++;
-        D.ba[g * PAC_NB + b] = (uint8_t)a;
-        D.sf[g * PAC_NB + b] = (uint8_t)r.read(4);
+        const uint32_t sfv = r.read(4);
+        if (valid) {
+            D.ba[g * PAC_NB + b] = (uint8_t)a;
+            D.sf[g * PAC_NB + b] = (uint8_t)sfv;
+        }
         bit += 8;
-        if (!a) continue;
+        if (!__ballot(a != 0)) continue;   // no lane codes the band
         const int lo = T->lower[b], nl = T->nlines[b];
-        if (!master) {
-            for (int l = lo; l < lo + nl; ++l) codes[dec_code_at(0, l)] = (uint16_t)r.read(a);
-            bit += (int64_t)nl * a;
-        } else {
-            DecBits sg;                            // nl sign bits, then nl Huffman codes
+        DecBits sg;                        // master: nl sign bits, then nl Huffman codes
+        if (master && a) {
             sg.init(p + 4, bit, end);
             r.advance(nl);
             bit += nl;
-            const int tid = id < 0 ? 0 : (id >= PAC_NTAB ? PAC_NTAB - 1 : id);
-            for (int l = lo; l < lo + nl; ++l) {
-                const uint32_t sym = dec_huff(r, htab, hd, stab, tid, a);
-                codes[dec_code_at(0, l)] = (uint16_t)(sym + (sg.read(1) << (a - 1)));
-            }
-            bit = -1;                              // recomputed below from the main reader
         }
-        if (bit < 0) bit = bits_consumed(r, p + 4);
+        for (int l = lo; l < lo + nl; ++l) {
+            if (l / DEC_GRP != gcur) {     // a new group: write the previous one
+                flush();
+                gcur = l / DEC_GRP;
+            }
+            if (a) {
+                uint32_t c;
+                if (!master) {
+                    c = r.read(a);
+                } else {
+                    const uint32_t sym = dec_huff(r, htab, hd, stab, tid, a);
+                    c = sym + (sg.read(1) << (a - 1));
+                }
+                st[l % DEC_GRP] = (uint16_t)c;
+            }
+        }
+        if (a) bit = master ? bits_consumed(r, p + 4) : bit + (int64_t)nl * a;
     }
-    if (master)
-        for (int b = 0; b < PAC_NB; ++b) D.lrms[g * PAC_NB + b] = (uint8_t)r.read(1);
-    if (D.bsf) D.bsf[g] = (uint8_t)r.read(1);
-    if (bits_consumed(r, p + 4) > 8 * (int64_t)nbytes) atomicOr(D.err, 1);
+    flush();
+    if (master) {
+        for (int b = 0; b < PAC_NB; ++b) {
+            const uint32_t f = r.read(1);
+            if (valid) D.lrms[g * PAC_NB + b] = (uint8_t)f;
+        }
+    }
+    if (D.bsf) {
+        const uint32_t f = r.read(1);
+        if (valid) D.bsf[g] = (uint8_t)f;
+    }
+    if (valid && bits_consumed(r, p + 4) > 8 * (int64_t)nbytes) atomicOr(D.err, 1);
 }
 
 // vDequantize (quantize.py:345-376) + vDequantizeUniform (:118-145), 4 scale bits

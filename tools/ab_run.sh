@@ -1,10 +1,16 @@
 #!/bin/bash
-# one GPU session of A/B experiments (edited per experiment; outputs under gpurun_out/)
+# one GPU session (edited per experiment; outputs under gpurun_out/)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-for v in seg32 seg64; do
-PAC_LIB=variants/libpacgpu_$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "decode or dec or reference or wav or bs" > gpurun_out/t_$v.log 2>&1 || { tail -30 gpurun_out/t_$v.log; exit 1; }
-echo "$v tests: $(tail -1 gpurun_out/t_$v.log)"
-done
-AB_ARGS="--mode decode" bash tools/ab_bench.sh head seg32 seg64 head seg32 seg64 || exit 1
-AB_ARGS="--mode decode --config 3" bash tools/ab_bench.sh head seg32 seg64 || exit 1
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/chk_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/chk_tests.log; exit 1; }
+echo "tests: $(tail -1 gpurun_out/chk_tests.log)"
+timeout -k 10 200 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+echo "smoke ok"
+run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err || { echo "bench $name failed"; tail -5 gpurun_out/bench_$name.err; exit 1; }; echo "bench $name: $(grep -o '"value": [0-9.]*' gpurun_out/bench_$name.json | head -1)"; }
+run config2 --steps 5 --warmup 1
+run config1 --config 1
+run config3 --config 3
+run config4 --config 4
+run decode --mode decode
+echo BENCH_DONE

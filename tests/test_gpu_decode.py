@@ -75,6 +75,22 @@ def test_multi_stream_round_trip_vs_oracle(ctx, prof):
         assert g.shape[0] >= n
 
 
+@pytest.mark.parametrize("prof", [pacfile.PROFILE_ORIGIN, pacfile.PROFILE_MASTER])
+def test_parse_and_synthesis_boundaries(ctx, prof):
+    """Channel-block counts across the parse's 512-lane workgroups and 64-lane
+    code tiles (lanes past the last channel-block stay in the wave-uniform line
+    loops) and streams across the synthesis' 64-block segments: 3 streams of
+    130, 66 and 65 hops (+ the flush block) = 528 stereo channel-blocks"""
+    fs = 48000
+    lens = [130 * 1024, 66 * 1024 - 5, 65 * 1024]
+    streams = [synth.pink_tones_pcm(n, fs, seed=10 + i) for i, n in enumerate(lens)]
+    secs = pacfile.encode_streams(streams, fs, prof, context=ctx)
+    got = pacfile.decode_streams(secs, fs, 2, prof, context=ctx)
+    o = P.Oracle(fs, huffman=(prof == pacfile.PROFILE_MASTER))
+    for n, sec, g in zip(lens, secs, got):
+        assert np.array_equal(g, o.decode_data(prof, sec, 2)), n
+
+
 def test_read_data_block_surface(ctx, tmp_path):
     """PACFile.ReadDataBlock hop by hop (the reference's decode driver loop,
     skipping the first result) written through PCMFile gives decode_file's bytes"""

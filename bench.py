@@ -459,9 +459,7 @@ def bench_decode(a, dist, ctx, job):
                    "profile": a.profile, "streams_per_gpu": job.ns, "blocks_per_stream": a.blocks_per_stream,
                    "global_blocks": int(total_blocks),
                    "parallelism": "streams sharded, %d rank(s)" % dist.world},
-        "roofline": {"bound": "hbm", "kernel": "k_dec_parse + k_dec_synth", "achieved": alg / dec_s / 1e9,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / dec_s / 1e9 / HBM_PEAK_GBS,
-                     "traffic": None},
+        "roofline": dec_roofline(alg, dec_s, job.blocks),
         "kernels_ms": {"parse": float(np.mean(parse_ms)), "synth": float(np.mean(synth_ms))},
         "bitstream_bytes_per_gpu": in_bytes,
         "src_hash": _build.source_hash(),
@@ -471,6 +469,27 @@ def bench_decode(a, dist, ctx, job):
     ctx.free(pcm_out)
     if dist.rank == 0:
         print(json.dumps(res))
+
+
+def dec_roofline(alg, dec_s, blocks):
+    """The decode line's roofline: algorithmic bytes (bitstream read + int16
+    PCM written) over the parse + synthesis time of one step, and the PMC HBM
+    bytes of the same two kernels (profiles/r*_decode_pmc.json, same source
+    hash only) per step."""
+    r = {"bound": "hbm", "kernel": "k_dec_parse + k_dec_synth", "achieved": alg / dec_s / 1e9,
+         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / dec_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+         "traffic_unit": "HBM bytes per step (one launch of each kernel: 2 x FETCH_SIZE + WRITE_SIZE)"}
+    per_block, srcs = 0.0, []
+    for k in ("k_dec_parse", "k_dec_synth"):
+        m, src = measured_profile("decode", k)
+        if m is None:
+            r["traffic_source"] = src
+            return r
+        per_block += m["hbm_read_bytes_per_block"] + m["hbm_write_bytes_per_block"]
+        srcs.append(src)
+    r.update({"traffic": per_block * blocks, "traffic_per_block": per_block,
+              "traffic_over_alg": per_block * blocks / alg, "traffic_source": srcs[0]})
+    return r
 
 
 def cpu_decode(ctx, p, out_dev, so, pcm_out, fo, a):

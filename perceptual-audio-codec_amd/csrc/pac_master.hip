@@ -219,6 +219,11 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
                                          double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
                                          int tid, long long* pm, int mk) {
     const int lane = tid & (WAVE - 1);
+    // wave priority: the barrier-bound list building above the barrier-free
+    // masking rows, so that a workgroup's waves reach its barriers sooner
+    // while the rows of the other workgroups fill the issue slots (thr −2.5 %;
+    // the tail and the emission, which co-run latency-bound, at 3)
+    __builtin_amdgcn_s_setprio(1);
     grp_variant_pow_store<FRONT_NT>(p, buf, tid);
     TPROF(mk);
     const MaskerLists L = masker_lists(buf, tmp);
@@ -228,6 +233,7 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
     int* rowctr = L.misc;
     if (tid == 0) *rowctr = 0;
     lds_sync();
+    __builtin_amdgcn_s_setprio(0);
 #pragma unroll 1
     while (true) {
         int k = 0;
@@ -1137,6 +1143,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     uint8_t (*sf_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + 2 * PAC_NB * WAVE * 8 + PAC_NB * WAVE);
     int* nl_s = reinterpret_cast<int*>(tail_lds + 2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE);
     const int lane = threadIdx.x;
+    __builtin_amdgcn_s_setprio(3);    // beside k_master_thr's waves (see thr_variant)
     if (lane < PAC_NB) nl_s[lane] = T->nlines[lane];
     wave_sync();                                       // one wave per workgroup; afterwards lanes touch only their columns
     const int sl = blockIdx.x * WAVE + lane;
@@ -1433,6 +1440,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const PacTables* __restrict__ T, const PacHuffTables* __restrict__ H, const uint64_t* __restrict__ hcode,
     PacMasterChunkBuf K, PacMasterFields F, const int64_t* __restrict__ blk_off, PacMasterChunk ck) {
     const int lane = threadIdx.x;
+    __builtin_amdgcn_s_setprio(3);    // beside k_master_thr's waves (see thr_variant)
     const int nch = ck.nch;
     const int64_t q = (int64_t)blockIdx.x * WAVE + lane;      // chunk-local channel-block: j nch + ch
     const int64_t j = q / nch;

@@ -2,10 +2,5 @@
 # one GPU session (edited per experiment; outputs under gpurun_out/)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err || { echo "bench $name failed"; tail -5 gpurun_out/bench_$name.err; exit 1; }; echo "bench $name: $(grep -o '"value": [0-9.]*' gpurun_out/bench_$name.json | head -1)"; }
-run config2 --steps 5 --warmup 1
-run config1 --config 1
-run config3 --config 3
-run config4 --config 4
-run decode --mode decode
-echo BENCH_DONE
+PAC_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --streams 4000 --steps 3 --warmup 1 --no-cpu > gpurun_out/rank2.json 2> gpurun_out/rank2.err || { tail -20 gpurun_out/rank2.err; exit 1; }
+tail -1 gpurun_out/rank2.json | cut -c1-200

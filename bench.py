@@ -94,7 +94,10 @@ def parse():
     ap.add_argument("--copies", type=int, default=1000, help="config 3: copies of every input file")
     ap.add_argument("--sample-rate", type=int, default=48000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="bounded CPU-baseline sample (oracle on host cores)")
+                    help="decode mode: bounded CPU-baseline sample (oracle on host cores)")
+    ap.add_argument("--cpu-blocks", type=int, default=-1,
+                    help="encode CPU baseline: blocks per sampled stream (default -1: whole streams, "
+                         "~10-15 s on 16 host threads for configs[2])")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the CPU baseline (default: the CPUs this process may run on, "
                          "os.sched_getaffinity, capped by OMP_NUM_THREADS when the host sets it -- the "
@@ -186,6 +189,15 @@ KERNEL_IO_BYTES = {
 }
 
 
+def chunk_blocks_of(bs):
+    """run_master's chunk size: PAC_CHUNK_BLOCKS, else 32768 (65536 with block
+    switching) -- pac_abi.hip run_master"""
+    env = os.environ.get("PAC_CHUNK_BLOCKS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return 65536 if bs else 32768
+
+
 def master_launches(nb, chunk_blocks=32768):
     """launches of each pass-1 master kernel per pac_encode_streams call of
     streams with nb[i] blocks: one per chunk (run_master in pac_abi.hip:
@@ -219,20 +231,85 @@ def measured_profile(kind, kernel):
     rel = os.path.relpath(files[-1], ROOT)
     if d.get("src_hash") != _build.source_hash():
         return None, "%s is stale (src_hash %s, this build %s)" % (rel, d.get("src_hash"), _build.source_hash())
-    k = d.get("kernels", {}).get(kernel)
+    k = d.get("kernels", {}).get(kernel) or d.get("kernels", {}).get("void " + kernel)   # templates: "void k<..>"
     if not k or not k.get("derived"):
         return None, "%s has no counters for %s" % (rel, kernel)
     out = dict(k["derived"])
+    c = k.get("pmc_total") or {}
+    if "waves_per_simd" not in out and c.get("SQ_WAVE_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+        out["waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)   # summarize_pmc.py
     out["_file"] = rel
     return out, rel
 
 
-def cpu_baseline(ctx, samples, fs, seconds, profile, threads, bs=False):
+def binding(dom, prof):
+    """What binds the dominant kernel, only as far as its same-hash PMC
+    profile shows it: VALU issue near saturation -> the VALU pipe (FP64 work
+    for the threshold kernels); otherwise unknown (null)."""
+    if not prof or prof.get("valu_issue_util") is None:
+        return None
+    u = prof["valu_issue_util"]
+    if u < 0.6:
+        return {"resource": None, "valu_issue_util": u,
+                "note": "%s issues VALU %.0f %% of its cycles: latency/occupancy bound, not VALU" % (dom, 100 * u)}
+    return {"resource": "fp64-valu" if prof.get("fp64_share_of_valu", 0) > 0.3 else "valu",
+            "valu_issue_util": u, "fp64_share_of_valu": prof.get("fp64_share_of_valu"),
+            "note": "%s issues VALU %.0f %% of its cycles (same-hash PMC): bound by VALU issue, not by HBM -- "
+                    "the HBM fraction is small by construction (SURVEY.md 8(d), DESIGN.md section 4)"
+                    % (dom, 100 * u)}
+
+
+# kernels whose occupancy the line reports beside the dominant one
+OCC_KERNELS = ["k_master_lrms_spec", "k_master_front", "k_master_tail", "k_origin_front", "k_master_thr_short"]
+
+
+def kernel_resources():
+    """the compiler's per-kernel VGPRs / LDS / occupancy limit of this build
+    (build.py writes it beside the library), {} when missing or stale"""
+    try:
+        with open(_build.RESOURCES) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    return d.get("kernels", {}) if d.get("src_hash") == _build.source_hash() else {}
+
+
+def occupancy(kind, kernels):
+    """Per-GPU occupancy (SURVEY 8(d) "Reported", BASELINE configs[4]): the
+    achieved resident waves per SIMD of each kernel from the same-hash PMC
+    profile (4 x SQ_WAVE_CYCLES / (SIMDs x the kernel's own cycles)), beside
+    the limit its resources allow (compiler report: VGPRs; LDS per CU)"""
+    res = kernel_resources()
+    out = {"unit": "resident waves per SIMD (of 8 slots), averaged over the kernel's own busy time",
+           "source": None, "kernels": {}}
+    for k in kernels:
+        name = k
+        r = res.get(k) or next((v for n, v in res.items() if n.startswith(k + "<true>")), None) or \
+            next((v for n, v in res.items() if n.startswith(k + "<")), {})
+        m, src = measured_profile(kind, k)
+        if m is None:
+            m, src2 = measured_profile(kind, k + "<true>")
+            if m is not None:
+                src, name = src2, k + "<true>"
+        e = {"achieved_waves_per_simd": m.get("waves_per_simd") if m else None,
+             "valu_issue_util": m.get("valu_issue_util") if m else None,
+             "limit_waves_per_simd": r.get("occupancy_waves_per_simd"), "vgprs": r.get("vgprs"),
+             "lds_bytes_per_workgroup": r.get("lds_bytes")}
+        lds = r.get("lds_bytes") or 0
+        if lds and k not in ("k_master_tail", "k_master_emit"):     # 256-thread workgroups: 4 waves, one per SIMD
+            e["lds_limit_waves_per_simd"] = min(8, (160 * 1024) // lds)
+        if m is not None:
+            out["source"] = src
+        out["kernels"][name] = e
+    return out
+
+
+def cpu_baseline(ctx, samples, fs, profile, threads, bs=False, max_blocks=-1):
     """The CPU oracle (oracle/pac_oracle.c) on a bounded sample of the same
-    workload, one host thread per stream (ctypes releases the GIL; the C
-    oracle keeps no global state): thread t encodes growing prefixes of its
-    stream (int16 frames copied back from HBM) until `seconds` have passed.
-    Returns the baseline and each thread's last (longest) data section."""
+    workload, one host thread per sampled stream (ctypes releases the GIL; the
+    C oracle keeps no global state): thread t encodes its whole stream (int16
+    frames copied back from HBM; at most max_blocks blocks when >= 0).
+    Returns the baseline and each thread's data section (the parity sample)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as P
     from concurrent.futures import ThreadPoolExecutor
@@ -245,28 +322,34 @@ def cpu_baseline(ctx, samples, fs, seconds, profile, threads, bs=False):
         o = P.Oracle(fs, huffman=(prof == P.MASTER), block_switch=bs)
         pcm = samples[t]
         full = (pcm.shape[0] + 1023) // 1024 + 1
-        done, chunk, last = 0, 16, b""
-        while time.perf_counter() - t0 < seconds and done < 200000:
-            n = min(chunk, full)
-            last = o.encode_data(prof, pcm, max_blocks=n)
-            done += n
-            if n == full:
-                break
-            chunk = min(chunk * 2, full)
-        return done, last
+        n = full if max_blocks < 0 else min(full, max_blocks)
+        return n, o.encode_data(prof, pcm, max_blocks=n)
 
     with ThreadPoolExecutor(threads) as ex:
-        res = list(ex.map(work, range(threads)))
+        res = list(ex.map(work, range(len(samples))))
     el = time.perf_counter() - t0
     done = sum(r[0] for r in res)
     base = {"value": done / el, "unit": "blocks/s", "cores": threads, "kind": "port",
             "host_cpus_visible": len(os.sched_getaffinity(0)),
             "reference_python": REF_PYTHON[profile],
             "sample": "oracle/pac_oracle.c (C restatement, byte-exact on the 16 reference "
-                      "fixtures), %s profile%s, %d host threads (one stream each, growing prefixes), "
-                      "%d stereo blocks of the same streams in %.1f s"
-                      % (profile, " + block switching" if bs else "", threads, done, el)}
+                      "fixtures), %s profile%s, %d host threads, one sampled stream each (whole streams%s), "
+                      "%d stereo blocks in %.1f s"
+                      % (profile, " + block switching" if bs else "", threads,
+                         "" if max_blocks < 0 else ", <= %d blocks" % max_blocks, done, el)}
     return base, [r[1] for r in res]
+
+
+def sample_streams(ns, n):
+    """n stream indices spread over a batch of ns: the first and the last, the
+    one-lane reservoir tail's wave boundaries (lanes 63/64 and 4095/4096 --
+    equal-length streams keep their index order in run_master's length sort),
+    then an even stride"""
+    pick = []
+    for i in [0, ns - 1, 63, 64, 4095, 4096] + [int(x) for x in np.linspace(0, ns - 1, max(n, 2))]:
+        if 0 <= i < ns and i not in pick and len(pick) < n:
+            pick.append(i)
+    return sorted(pick)
 
 
 def channel_blocks(b):
@@ -279,12 +362,12 @@ def channel_blocks(b):
     return out
 
 
-def parity_check(ctx, out_dev, starts, oracle_prefixes):
-    """The oracle's bytes for the first blocks of the sampled streams against
-    the GPU's bytes for the same streams: channel-blocks compared and how many
-    differ (flip rate)."""
+def parity_check(ctx, out_dev, starts, oracle_sections, streams):
+    """The oracle's bytes for the sampled streams against the GPU's bytes for
+    the same streams: channel-blocks compared and how many differ (SURVEY 8(d):
+    flip rate)."""
     checked = bad = 0
-    for st, ref in zip(starts, oracle_prefixes):
+    for st, ref in zip(starts, oracle_sections):
         if not ref:
             continue
         got = np.empty(len(ref), dtype=np.uint8)
@@ -292,8 +375,8 @@ def parity_check(ctx, out_dev, starts, oracle_prefixes):
         a, b = channel_blocks(ref), channel_blocks(got.tobytes())
         checked += len(a)
         bad += sum(1 for x, y in zip(a, b) if x != y) + max(0, len(a) - len(b))
-    return {"checked_channel_blocks": checked, "mismatching": bad,
-            "against": "oracle/pac_oracle.c on the CPU-baseline sample"}
+    return {"checked_channel_blocks": checked, "mismatching": bad, "streams": streams,
+            "against": "oracle/pac_oracle.c on the CPU-baseline sample (the sampled streams, whole)"}
 
 
 class Job:
@@ -322,10 +405,10 @@ class Job:
         self.ctx.free(self.out_dev)
         self.ctx.free(self.pcm_dev)
 
-    def cpu_samples(self, nt, max_frames=4096 * 1024):
-        """int16 frames of the first nt streams (copied back from HBM)"""
+    def cpu_samples(self, idx, max_frames=4096 * 1024):
+        """int16 frames of the streams idx (copied back from HBM)"""
         out = []
-        for t in range(min(nt, self.ns)):
+        for t in idx:
             n = min(int(self.fo[t + 1] - self.fo[t]), max_frames)
             pcm = np.empty((n, 2), dtype=np.int16)
             self.ctx.to_host(pcm, self.pcm_dev + int(self.fo[t]) * 4)
@@ -364,8 +447,8 @@ class WavJob(Job):
         self.ctx.free(self.out_dev)
         self.ctx.free(self.blob_dev)
 
-    def cpu_samples(self, nt, max_frames=4096 * 1024):
-        return [fr[:max_frames] for fr in self.frames_host[:nt]]
+    def cpu_samples(self, idx, max_frames=4096 * 1024):
+        return [self.frames_host[t][:max_frames] for t in idx]
 
 
 def synthetic_job(a, ctx, rank):
@@ -566,10 +649,14 @@ def main():
 
     def step():
         ms = {f: 0.0 for f, _ in PHASES["bs" if a.bs else a.profile]}
+        chunks = repacked = 0
         for j in jobs:
             t = j.run()
             for f in ms:
                 ms[f] += getattr(t, f)
+            chunks += t.chunks
+            repacked += t.repacked
+        ms["_chunks"], ms["_repacked"] = chunks, repacked
         return ms
 
     for _ in range(a.warmup):
@@ -601,7 +688,11 @@ def main():
     step_s = el_max / a.steps
     # algorithmic bytes = PCM read + bitstream written, per block
     alg_per_block = PCM_BYTES_PER_BLOCK + out_bytes / blocks
-    launches = sum(master_launches(j.bcounts) for j in jobs) if a.master and dom != "k_master_place" else len(jobs)
+    # launches of the dominant kernel per step: run_master's chunk count (pac_timing.chunks), checked
+    # against the host mirror of its chunk geometry
+    launches = int(per[-1]["_chunks"]) if a.master and dom != "k_master_place" else len(jobs)
+    if a.master and dom != "k_master_place":
+        assert launches == sum(master_launches(j.bcounts, chunk_blocks_of(a.bs)) for j in jobs), launches
     achieved = alg_per_block * blocks / dom_s / 1e9 if dom_s > 0 else 0.0
     prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
     traffic_pb = None
@@ -639,9 +730,7 @@ def main():
                          "(not algorithmic)",
         "step": {"achieved": alg_per_block * blocks / step_s / 1e9,
                  "frac": alg_per_block * blocks / step_s / 1e9 / HBM_PEAK_GBS},
-        "binding": {"resource": "fp64-valu", "executed_frac": fp64.get("executed_frac"),
-                    "note": "%s is bound by FP64 VALU issue (the masking sums), not by HBM: the HBM "
-                            "fraction is small by construction (SURVEY.md 8(d), DESIGN.md section 4)" % dom},
+        "binding": binding(dom, prof),
     }
     if a.config == 2:
         data = "synthetic (device-generated pink noise (Voss, counter hash) + 440/1250/5300 Hz tones)"
@@ -684,7 +773,9 @@ def main():
         "roofline": roofline,
         "fp64": fp64,
         "kernels_ms": kern_ms,
+        "occupancy": occupancy("bs" if a.bs else a.profile, [dom] + [k for k in OCC_KERNELS if k in kern_ms and k != dom]),
         "out_bytes_per_gpu": out_bytes,
+        "staging_repacked_calls": int(sum(p["_repacked"] for p in per)),
         "src_hash": _build.source_hash(),
     }
     if desc:
@@ -696,11 +787,12 @@ def main():
         # the CPU sample: the first streams of the (first) job, copied back from HBM
         j = jobs[0]
         nt = max(1, min(a.cpu_threads, j.ns))
-        samples = j.cpu_samples(nt)
-        starts = [int(j.so[t]) for t in range(len(samples))]
-        res["cpu_baseline"], prefixes = cpu_baseline(ctx, samples, j.p.sample_rate, a.cpu_seconds, a.profile, nt,
-                                                     bs=a.bs)
-        res["parity"] = parity_check(ctx, j.out_dev, starts, prefixes)
+        idx = sample_streams(j.ns, nt)
+        samples = j.cpu_samples(idx)
+        starts = [int(j.so[t]) for t in idx]
+        res["cpu_baseline"], sections = cpu_baseline(ctx, samples, j.p.sample_rate, a.profile, nt, bs=a.bs,
+                                                     max_blocks=a.cpu_blocks)
+        res["parity"] = parity_check(ctx, j.out_dev, starts, sections, idx)
     for j in jobs:
         j.free()
     if dist.rank == 0:

@@ -106,6 +106,9 @@ typedef struct {
                            default fused k_master_lrms_spec (LRMS + spectra; lrms_ms is then 0) */
     float emit_ms;      /* master: k_master_emit (the bitstream packing beside the next chunk's tail; pack_ms
                            is then k_master_place, the copy to the file offsets) */
+    int32_t chunks;     /* master: pass-1 chunks of the call = launches of each pass-1 kernel (run_master) */
+    int32_t repacked;   /* master: 1 if the tail's staging overflowed and the call re-ran through k_master_pack
+                           (~2x the encode time; pac_abi.hip pac_encode_streams) */
 } pac_timing;
 
 /* The codec.Encode() result of one block (codec.py:129 / Origin codec.py:67). */

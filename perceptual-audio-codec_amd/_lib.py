@@ -69,7 +69,7 @@ class Timing(C.Structure):
                 ("pack_ms", C.c_float), ("total_ms", C.c_float),
                 ("n_channel_blocks", C.c_int64), ("out_bytes", C.c_int64),
                 ("thr_ms", C.c_float), ("lrms_ms", C.c_float), ("thr_short_ms", C.c_float),
-                ("spec_ms", C.c_float), ("emit_ms", C.c_float)]
+                ("spec_ms", C.c_float), ("emit_ms", C.c_float), ("chunks", C.c_int32), ("repacked", C.c_int32)]
 
 
 class BlockFields(C.Structure):

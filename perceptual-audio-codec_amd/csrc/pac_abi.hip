@@ -983,6 +983,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipStreamWaitEvent(s3, e, 0));
     }
     const int64_t nck = (int64_t)chunks.size();
+    c->last.chunks = (int32_t)nck;
     auto bufset = [&](int64_t i) {
         const int64_t k = i % 3;
         return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
@@ -1153,6 +1154,7 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     const bool master = p->profile == PAC_PROFILE_MASTER;
     if (master && !c->have_huff) return set_err(PAC_E_TABLES, "master profile needs pac_huffman_load()");
     if (frame_offsets[0] != 0) return set_err(PAC_E_ARG, "frame_offsets[0] must be 0");
+    c->last = pac_timing{};        // this call's timing, chunk count and repack flag only
     for (int s = 0; s < n_streams; s++)
         if (frame_offsets[s + 1] < frame_offsets[s])
             return set_err(PAC_E_ARG, "frame_offsets must be non-decreasing");
@@ -1227,7 +1229,12 @@ extern "C" int pac_encode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         int64_t scap = 0;
         if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false, false, &need, &scap))) return rc;
         HIPCHK(hipStreamSynchronize(s));
+        c->last.repacked = 0;
+        if ((int64_t)need > scap && total > out_capacity)    // no second pass for an output that cannot fit
+            return set_err(PAC_E_CAPACITY, "output needs %lld bytes, capacity %lld", (long long)total,
+                           (long long)out_capacity);
         if ((int64_t)need > scap) {   // the staging overflowed (> 1.5 KB per channel-block): again, packing
+            c->last.repacked = 1;
             HIPCHK(hipMemcpyAsync(c->st_extra.p, ex.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(c->st_deposit.p, dp.data(), n_streams * sizeof(int64_t), hipMemcpyHostToDevice, s));
             if ((rc = run_master(c, p, T, src, blk, out_dev, out_capacity, &total, false, true))) return rc;

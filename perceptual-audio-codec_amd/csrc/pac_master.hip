@@ -1532,7 +1532,8 @@ __global__ __launch_bounds__(256) void k_master_place(PacMasterFields F, int64_t
     if (g >= G) return;
     const int nb = F.nbytes[g];
     const int64_t og = off[g], so = F.stoff[g];
-    if (og + nb > cap || so + nb > F.stg_cap) return;
+    // k_master_emit's padded size: a channel-block it skipped is skipped here too
+    if (og + nb > cap || so + (4 + ((nb - 4 + 3) & ~3)) > F.stg_cap) return;
     const uint8_t* src = F.stg + so;
     uint8_t* dst = out + og;
     for (int i = lane; i < nb; i += WAVE) dst[i] = src[i];

@@ -88,6 +88,12 @@ def derive(c, blocks, total_ms):
     if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
         # extra cycles / all LDS-array cycles (MI355X_MICROARCH.md LDS section)
         d["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    if "SQ_WAVE_CYCLES" in c and c.get("GRBM_GUI_ACTIVE"):
+        # achieved occupancy: resident waves per SIMD averaged over the kernel's
+        # busy time (SQ_WAVE_CYCLES counts quad-cycles, MI355X_MICROARCH.md;
+        # under --pmc the dispatches run one at a time, so GRBM_GUI_ACTIVE / 8
+        # is this kernel's own duration in cycles)
+        d["waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / 8)
     if "SQ_WAIT_ANY" in c and c.get("SQ_WAVE_CYCLES"):
         d["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
     return d

@@ -211,13 +211,14 @@ __device__ __forceinline__ uint32_t pac_mantissa(double x, int scale, int nMantB
 // pcmfile.py:89-98 + quantize.py:120-145: +-2|c|/65535, -32768 -> +0.0.
 // Branch-free; the quotient is RN(2|c|/65535) exactly: q0 = 2|c| * RN(1/65535)
 // corrected once by its fma residual (checked for every |c| <= 32768).
+// Rounding to nearest is odd-symmetric, so the signed code goes through the
+// same three operations (-32768 -> 0 first): RN(-x) = -RN(x), and 0 stays +0.0
+// (bit-identical to the sign-magnitude form for all 65536 codes).
 __device__ __forceinline__ double pac_pcm_to_float(int c) {
-    const int a = c == -32768 ? 0 : (c < 0 ? -c : c);
-    const double n = (double)(2 * a);
+    const double n = (double)(2 * (c == -32768 ? 0 : c));
     const double r = 1.0 / 65535.0;
-    double q = n * r;
-    q = __builtin_fma(__builtin_fma(-q, 65535.0, n), r, q);
-    return c < 0 && a != 0 ? -q : q;
+    const double q = n * r;
+    return __builtin_fma(__builtin_fma(-q, 65535.0, n), r, q);
 }
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {

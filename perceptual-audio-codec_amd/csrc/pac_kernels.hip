@@ -115,6 +115,28 @@ __device__ __forceinline__ double2 stereo_frame(const BlockPcm& r, int i) {
     return make_double2(pac_pcm_to_float((int)(int16_t)(w & 0xffffu)), pac_pcm_to_float((int)(int16_t)(w >> 16)));
 }
 
+// The block's stereo frames (int16 source) through a raw buffer resource
+// whose range is the stream's frames from the block's first in-stream frame
+// on: a frame past the stream's end, or before its start (the zero first
+// prior block), is out of the range and reads 0 -- no per-frame bounds test,
+// one 32-bit load per frame, and a block's offsets stay within 8 KB of the
+// base (the range check covers the VGPR and immediate offsets used here).
+struct StereoFrames {
+    __amdgpu_buffer_rsrc_t rs;
+    int off0;     // byte offset of frame 0 of the block (negative before the stream start)
+    __device__ __forceinline__ explicit StereoFrames(const BlockRef& r) {
+        const int64_t lo = r.first_frame > 0 ? r.first_frame : 0;
+        const int64_t n = r.n_frames - lo;
+        const int64_t bytes = n <= 0 ? 0 : (n >= (1ll << 29) ? (1ll << 31) : 4 * n);
+        rs = __builtin_amdgcn_make_buffer_rsrc((void*)(r.pcm + 2 * lo), 0, (int)bytes, 0x00020000);
+        off0 = (int)(4 * (r.first_frame - lo));
+    }
+    __device__ __forceinline__ double2 operator()(int i) const {
+        const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(rs, off0 + 4 * i, 0, 0);
+        return make_double2(pac_pcm_to_float((int)(short)(w & 0xffffu)), pac_pcm_to_float((int)w >> 16));
+    }
+};
+
 // sample i of channel u (0, 1) of a stereo block (r: the channel-0 BlockPcm of
 // an interleaved stereo source): one 16-bit load; zero outside the stream
 __device__ __forceinline__ double stereo_sample(const BlockPcm& r, int i, int u) {

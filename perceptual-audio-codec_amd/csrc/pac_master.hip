@@ -589,7 +589,8 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
                                            double2* bufB, double* __restrict__ mdct) {
     const int tid = threadIdx.x;
     const int64_t gb = cp.gb;
-    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockRef bL = locate_sb(src, cp.s, cp.t, gb, 0);
+    const BlockPcm rL(bL);
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
     // the leaf and band tables, loaded before the FFTs (their round trips
     // overlap the transform instead of following it)
@@ -616,8 +617,9 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         else nyA = X.x;
     };
     if (!rL.f) {
+        const StereoFrames sf(bL);
         grp_spectrum_cplx2p_put<256>([&](int n) {      // frames 2n, 2n+1: (L0, R0), (L1, R1)
-            const double2 f0 = stereo_frame(rL, 2 * n), f1 = stereo_frame(rL, 2 * n + 1);
+            const double2 f0 = sf(2 * n), f1 = sf(2 * n + 1);
             return make_double4(f0.x, f1.x, f0.y, f1.y);
         }, T, bufA, bufB, tid, put);
     } else {
@@ -730,7 +732,8 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
     const int64_t gb = cp.gb;
     const int fl = F.bsf ? F.bsf[gb] : 0;
     if (fl & PAC_BS_SHORT) return;                 // k_master_thr_short's
-    const BlockPcm rL(locate_sb(src, cp.s, cp.t, gb, 0));
+    const BlockRef bL = locate_sb(src, cp.s, cp.t, gb, 0);
+    const BlockPcm rL(bL);
     const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // mono: B = A, unused
     // bins -2..1026 at o[bin + 2], written by the real split straight from its
     // registers (no LDS round trip): the mirrored edge bins X[-k] = X[2048-k] =
@@ -743,9 +746,10 @@ __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables
         if (k == 1022 || k == 1023) q[2048 - k] = make_double2(X.x, -X.y);
     };
     if (ck.nch == 2 && !rL.f) {
+        const StereoFrames sf(bL);
         grp_spectrum_cplx2p_put<256>([&](int n) {   // frames 2n, 2n+1 of both channels, one load each
             const int i0 = 2 * n;
-            const double2 f0 = stereo_frame(rL, i0), f1 = stereo_frame(rL, i0 + 1);
+            const double2 f0 = sf(i0), f1 = sf(i0 + 1);
             const double2 h = *reinterpret_cast<const double2*>(T->hann + i0);
             const double2 w = fl ? make_double2(bs_long_win(T, fl, i0), bs_long_win(T, fl, i0 + 1))
                                  : *reinterpret_cast<const double2*>(T->sine + i0);

@@ -345,10 +345,13 @@ def sample_streams(ns, n):
     one-lane reservoir tail's wave boundaries (lanes 63/64 and 4095/4096 --
     equal-length streams keep their index order in run_master's length sort),
     then an even stride"""
-    pick = []
-    for i in [0, ns - 1, 63, 64, 4095, 4096] + [int(x) for x in np.linspace(0, ns - 1, max(n, 2))]:
-        if 0 <= i < ns and i not in pick and len(pick) < n:
-            pick.append(i)
+    pick = [i for i in dict.fromkeys([0, ns - 1, 63, 64, 4095, 4096]) if 0 <= i < ns][:n]
+    for k in range(n, 4 * n + 2):          # the stride, denser until n distinct indices
+        if len(pick) >= min(n, ns):
+            break
+        for x in np.linspace(0, ns - 1, k - len(pick) + 2)[1:-1]:
+            if int(round(x)) not in pick and len(pick) < n:
+                pick.append(int(round(x)))
     return sorted(pick)
 
 

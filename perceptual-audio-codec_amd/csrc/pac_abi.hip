@@ -157,6 +157,7 @@ static void build_tables(int fs, int window, PacTables* t) {
         double a = -2.0 * M_PI * k / 2048.0;
         t->rfft_tw[k] = make_double2(cos(a), sin(a));
     }
+    for (int k = 0; k < PAC_HALFN; k++) t->rfft_tw2[k] = make_double2(0.5 * t->rfft_tw[k].x, 0.5 * t->rfft_tw[k].y);
     t->sine_win = window == PAC_WINDOW_SINE;
     for (int k = 0; k < PAC_HALFN; k++) {
         // sin(pi (n + 1/2)/N) = (e^{i pi (n+1/2)/N} - e^{-i pi (n+1/2)/N}) / 2i turns the
@@ -365,6 +366,9 @@ struct pac_ctx {
     bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
     bool side_early = false;               // PAC_SIDE_EARLY=1: side(i+2) beside thr(i+1), spectra double-buffered
     bool tail_early = false;               // PAC_TAIL_EARLY=1: tail(i) right after front(i) (A/B switch)
+    bool front_late = false;               // PAC_FRONT_LATE=1: front(i) on s2 after side(i+1), beside thr(i+1)
+                                           // (thresholds double-buffered; measured slower: thr +135 ms for a
+                                           // side window -100 ms); default: on s0 beside side(i+1)
     int64_t stg_bias = 0;                  // PAC_DEBUG_STG_BIAS: staging starts this many bytes in (tests of >4 GB offsets)
     int64_t stg_cap_max = 0;               // PAC_DEBUG_STG_CAP: staging capacity cap (tests of the pack fallback)
     hipEvent_t evs[5] = {};                 // master: front/tail hand-off events (no timing)
@@ -412,6 +416,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_FRONT_FAST")) c->front_fast = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_EARLY")) c->side_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_TAIL_EARLY")) c->tail_early = atoi(f) != 0;
+    if (const char* f = getenv("PAC_FRONT_LATE")) c->front_late = atoi(f) != 0;
     if (const char* f = getenv("PAC_CHUNK_BLOCKS")) c->chunk_blocks = atoll(f);
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
@@ -890,7 +895,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure(cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure((c->side_early ? 2 : 1) * cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_thr.ensure((c->front_late ? 2 : 1) * cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure((c->side_early ? 2 : 1) * cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(3 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(3 * cbmax * 2 * PAC_NB)))
         return rc;
     pack = pack || dbg_codes;
@@ -984,9 +989,13 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     }
     const int64_t nck = (int64_t)chunks.size();
     c->last.chunks = (int32_t)nck;
+    // front(i) after side(i+1) on s2, beside thr(i+1) (thresholds double-buffered):
+    // the window between two threshold launches is the side kernel alone
+    const bool late = c->front_late && !c->side_early && !serial;
     auto bufset = [&](int64_t i) {
         const int64_t k = i % 3;
-        return PacMasterChunkBuf{c->m_thr.p, c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
+        return PacMasterChunkBuf{c->m_thr.p + (late ? (i & 1) * cbmax * 6 * PAC_HALFN : 0),
+                                 c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
                                  c->m_spec.p + (c->side_early ? (i & 1) * cbmax * 2 * PAC_SPEC_LD : 0),
                                  c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
@@ -1035,7 +1044,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         const PacMasterChunkBuf K = bufset(i);
         if (early) spec_ready = spec_ev[i];
         HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
-        if (i >= 3) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
+        if (i >= 3 && !late) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
         if ((rc = mark(0, -1))) return rc;
         hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0,
                            src_thr, T, K, F, q.ck);
@@ -1051,14 +1060,19 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             if ((rc = launch_side(i + 1))) return rc;
             spec_ready = event_on(s2);
         }
-        if ((rc = mark(0, -1))) return rc;
+        const hipStream_t sf = late ? s2 : s0;       // the front's stream
+        if (late) {
+            if (i + 1 >= nck) HIPCHK(hipStreamWaitEvent(s2, thr_done, 0));      // no side(i+1) before it
+            if (i >= 3) HIPCHK(hipStreamWaitEvent(s2, tail_done[i - 3], 0));   // set k's last reader
+        }
+        if ((rc = mark(late ? 2 : 0, -1))) return rc;
         if (front_fast)
-            hipLaunchKernelGGL(k_master_front<true>, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
+            hipLaunchKernelGGL(k_master_front<true>, dim3((unsigned)q.B), dim3(256), 0, sf, src_front, T, K, F, q.ck);
         else
-            hipLaunchKernelGGL(k_master_front<false>, dim3((unsigned)q.B), dim3(256), 0, s0, src_front, T, K, F, q.ck);
+            hipLaunchKernelGGL(k_master_front<false>, dim3((unsigned)q.B), dim3(256), 0, sf, src_front, T, K, F, q.ck);
         HIPCHK(hipGetLastError());
-        if ((rc = mark(0, 1))) return rc;
-        const hipEvent_t front_done = event_on(s0);
+        if ((rc = mark(late ? 2 : 0, 1))) return rc;
+        const hipEvent_t front_done = event_on(sf);
         if (early && i + 2 < nck) {                   // buffer set i & 1 is free once front(i) is done
             HIPCHK(hipStreamWaitEvent(s2, front_done, 0));
             if ((rc = launch_side(i + 2))) return rc;

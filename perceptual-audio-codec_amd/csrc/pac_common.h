@@ -29,6 +29,7 @@ struct PacTables {
     // fft_tw, so a kernel reaches them from the same pointer
     double2 fft_tw4[3 * (4 + 16 + 64 + 256)];
     double2 rfft_tw[PAC_HALFN];        // exp(-2 pi i k / 2048), k < 1024
+    double2 rfft_tw2[PAC_HALFN];       // exp(-2 pi i k / 2048) / 2 (the side kernel's fused split)
     double bark_line[PAC_HALFN];  // Bark(MDCTFreqs)                psychoac.py:434,95
     double tiq[PAC_HALFN];        // Intensity(Thresh(MDCTFreqs))   psychoac.py:437
     double bark_bin[PAC_HALFN];   // Bark(k * (fs//N))              psychoac.py:186-188
@@ -224,4 +225,9 @@ __device__ __forceinline__ double pac_pcm_to_float(int c) {
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(__dsub_rn(__dmul_rn(a.x, b.x), __dmul_rn(a.y, b.y)),
                         __dadd_rn(__dmul_rn(a.x, b.y), __dmul_rn(a.y, b.x)));
+}
+// a * b with two fused multiply-adds (4 VALU instead of 6): the side kernel's
+// paired FFTs (rounding of the same class, not bit-identical to cmul)
+__device__ __forceinline__ double2 cmul_fma(double2 a, double2 b) {
+    return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
 }

@@ -506,17 +506,18 @@ __device__ __forceinline__ void grp_spectrum_cplx2p_put(const D4& d4, const PacT
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const double2* Z = u ? bufB : bufA;
+            // X[k] = (Z[k] + conj Z[-k])/2 - i W^k (Z[k] - conj Z[-k])/2: the halves folded into
+            // rfft_tw2 and the final fused multiply-adds
+            const double2 A0 = Z[kk[0]], A1 = Z[kk[1]];
+            const double2 B0 = p ? A1 : A0, B1 = p ? A0 : A1;        // Z[(1024 - k) & 1023]
             double2 X[2];
 #pragma unroll
             for (int side = 0; side < 2; ++side) {
-                const double2 A = Z[kk[side]];
-                const double2 Bc = Z[(1024 - kk[side]) & 1023];
-                const double2 e = make_double2(0.5 * (A.x + Bc.x), 0.5 * (A.y - Bc.y));
-                const double2 o = make_double2(0.5 * (A.x - Bc.x), 0.5 * (A.y + Bc.y));
-                const double2 wo = cmul(T->rfft_tw[kk[side]], o);
-                X[side] = make_double2(e.x + wo.y, e.y - wo.x);
+                const double2 A = side ? A1 : A0, Bc = side ? B1 : B0;
+                const double2 wo = cmul_fma(T->rfft_tw2[kk[side]], make_double2(A.x - Bc.x, A.y + Bc.y));
+                X[side] = make_double2(__builtin_fma(0.5, A.x + Bc.x, wo.y), __builtin_fma(0.5, A.y - Bc.y, -wo.x));
             }
-            if (p == 0) put(u, 1024, make_double2(Z[0].x - Z[0].y, 0.0));
+            if (p == 0) put(u, 1024, make_double2(A0.x - A0.y, 0.0));
             put(u, kk[0], X[0]);
             put(u, kk[1], X[1]);
         }

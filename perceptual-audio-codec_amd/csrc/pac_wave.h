@@ -294,7 +294,8 @@ __device__ __forceinline__ void grp_fft_stockham_1buf(double2* buf, const double
 
 // Two independent one-buffer Stockham FFTs (buffers a and b) advanced stage by
 // stage together: each thread's butterflies of both in flight, one pair of
-// barriers per stage for both.  Bit-identical to grp_fft_stockham_1buf on each.
+// barriers per stage for both.  grp_fft_stockham_1buf's arithmetic with the
+// twiddle products as fused multiply-adds (cmul_fma).
 // The first stage takes its inputs from ld(n) = (a[n], b[n]) as a double4
 // (the staged sample pairs, computed from global memory) instead of LDS: no
 // staging pass and no first-stage barriers (the caller guarantees that no
@@ -334,9 +335,9 @@ __device__ __forceinline__ void grp_fft_stockham_1buf_x2(double2* a, double2* b,
                     v[u][q][2] = bufs[u][(j + 2 * N4) ^ xj ^ fft_swz(2 * N4)];
                     v[u][q][3] = bufs[u][(j + 3 * N4) ^ xj ^ fft_swz(3 * N4)];
                     const double2* w = tw4_of(tw, Ns, k);
-                    v[u][q][1] = cmul(v[u][q][1], w[0]);
-                    v[u][q][2] = cmul(v[u][q][2], w[1]);
-                    v[u][q][3] = cmul(v[u][q][3], w[2]);
+                    v[u][q][1] = cmul_fma(v[u][q][1], w[0]);
+                    v[u][q][2] = cmul_fma(v[u][q][2], w[1]);
+                    v[u][q][3] = cmul_fma(v[u][q][3], w[2]);
                 }
             grp_sync<NT>();
         }

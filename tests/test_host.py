@@ -332,3 +332,43 @@ def test_bench_dist_gloo_world2(tmp_path):
                         str(script)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.strip().splitlines() == ["MAX 2.5 SUM 3.0"]
+
+
+def _bench_module():
+    import importlib.util
+    saved = sys.argv
+    sys.argv = ["bench.py"]
+    try:
+        spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+        b = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(b)
+    finally:
+        sys.argv = saved
+    return b
+
+
+def test_bench_parity_sample_spans_the_batch():
+    """bench.py's CPU-baseline / parity sample: first and last stream, the
+    one-lane tail's wave boundaries, then an even stride."""
+    b = _bench_module()
+    idx = b.sample_streams(10000, 16)
+    assert len(idx) == 16 and idx == sorted(set(idx))
+    assert {0, 63, 64, 4095, 4096, 9999} <= set(idx)
+    assert max(np.diff(idx)) < 1000
+    assert b.sample_streams(22, 16)[-1] == 21 and len(b.sample_streams(22, 16)) == 16
+    assert b.sample_streams(3, 16) == [0, 1, 2]
+
+
+def test_bench_chunk_geometry_mirror(monkeypatch):
+    """bench.py mirrors run_master's chunk count (the line's launches_per_step,
+    checked against pac_timing.chunks on the GPU): 32768-block chunks, 65536
+    with block switching, PAC_CHUNK_BLOCKS overrides."""
+    b = _bench_module()
+    monkeypatch.delenv("PAC_CHUNK_BLOCKS", raising=False)
+    assert b.chunk_blocks_of(False) == 32768 and b.chunk_blocks_of(True) == 65536
+    monkeypatch.setenv("PAC_CHUNK_BLOCKS", "7")
+    assert b.chunk_blocks_of(True) == 7
+    assert b.master_launches([1000] * 10000, 32768) == 334       # S = 3: ceil(1000 / 3)
+    assert b.master_launches([1000] * 12500, 65536) == 200       # S = 5
+    # ragged: 10, 4, 1 blocks in chunks of 4: S = 1 (3 running), 2, 2 (2 running), 4, 1 (one left)
+    assert b.master_launches([10, 4, 1], 4) == 5

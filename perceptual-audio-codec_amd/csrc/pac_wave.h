@@ -1201,17 +1201,17 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
         }
     }
     RP_T(t3);
+    // the direct terms in the line's own form, B_m + ku_m ((z_l - z_m) - 1/2) --
+    // the reference's (|dz| - 1/2) slope product (psychoac.py:111-116) -- one
+    // fused multiply-add fewer than the row-middle form the moment form needs
     if (direct) {
 #pragma unroll 2
-        for (int m = m0; m < ua; ++m) {             // m < umin <= Ul on every lane
-            const double ku = L.lku[m];
-            up += pac_exp2_v(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
-        }
+        for (int m = m0; m < ua; ++m)               // m < umin <= Ul on every lane
+            up += pac_exp2_v(__builtin_fma((zl - L.lz[m]) - 0.5, L.lku[m], L.lB[m]));
     }
 #pragma unroll 2
     for (int m = ua; m < umax; ++m) {
-        const double ku = L.lku[m];
-        const double t = pac_exp2_v(__builtin_fma(dl, ku, __builtin_fma((zm - L.lz[m]) - 0.5, ku, L.lB[m])));
+        const double t = pac_exp2_v(__builtin_fma((zl - L.lz[m]) - 0.5, L.lku[m], L.lB[m]));
         up += (m < Ul) ? t : 0.0;
     }
     RP_T(t4);

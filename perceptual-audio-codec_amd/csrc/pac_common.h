@@ -175,38 +175,37 @@ __device__ __forceinline__ double pac_spl(double I) {
     return s < -30.0 ? -30.0 : s;
 }
 
-// QuantizeUniform (quantize.py:40-64) for |a|, R bits
-__device__ __forceinline__ uint64_t pac_quant_abs(double a, int R) {
-    uint64_t sbm = 1ull << (R - 1);
-    double largest = (double)(sbm << 1) - 1.0;
+// QuantizeUniform (quantize.py:40-64) for |a|, R <= 31 bits: the code is below
+// 2^(R-1) <= 2^30, so 32-bit integers carry it (one v_cvt_u32_f64; the
+// float64 -> uint64 conversion is a ~10-instruction sequence)
+__device__ __forceinline__ uint32_t pac_quant_abs32(double a, int R) {
+    const uint32_t sbm = 1u << (R - 1);
     if (a >= 1.0) return sbm - 1;
-    return (uint64_t)(__dadd_rn(__dmul_rn(largest, a), 1.0) / 2.0);
+    const double largest = (double)(2u * sbm - 1u);
+    return (uint32_t)(__dadd_rn(__dmul_rn(largest, a), 1.0) * 0.5);    // / 2.0, exact
 }
+__device__ __forceinline__ uint64_t pac_quant_abs(double a, int R) { return pac_quant_abs32(a, R); }
 
-// ScaleFactor (quantize.py:148-177) with nScaleBits = 4
+// ScaleFactor (quantize.py:148-177) with nScaleBits = 4: the leading zeros of
+// the R-bit code (q << 1 < 2^R), capped at 15 -- by count-leading-zeros
+// instead of the reference's shift loop (the same value)
 __device__ __forceinline__ int pac_scale_factor(double a, int nMantBits) {
     if (nMantBits <= 0) return 0;
-    const int largestScale = 15;
-    int R = nMantBits + largestScale;
-    uint64_t q = pac_quant_abs(fabs(a), R) << 1;
-    // leading zeros of the R-bit code, capped at 15
-    int scale = 0;
-    uint64_t zmask = 1ull << (R - 1);
-    while (scale < largestScale && (zmask & q) == 0) { q <<= 1; scale++; }
-    return scale;
+    const int R = nMantBits + 15;
+    const uint32_t q = pac_quant_abs32(fabs(a), R) << 1;
+    const int lz = q ? __builtin_clz(q) - (32 - R) : R;
+    return lz < 15 ? lz : 15;
 }
 
-// vMantissa (quantize.py:315-342) for one line, nScaleBits = 4
+// vMantissa (quantize.py:315-342) for one line, nScaleBits = 4:
+// (code << (scale + 1)) >> (R - nMantBits + 1) = code >> (15 - scale) for
+// scale <= 15 (the code is below 2^30: no bits pass bit 31)
 __device__ __forceinline__ uint32_t pac_mantissa(double x, int scale, int nMantBits) {
-    const int R = nMantBits + 15;
-    bool sign = __builtin_signbit(x);
-    double a = sign ? -x : x;
-    uint64_t sbm = 1ull << (R - 1);
-    double largest = (double)(sbm << 1) - 1.0;
-    uint64_t code = (a < 1.0) ? (uint64_t)(__dadd_rn(__dmul_rn(a, largest), 1.0) / 2.0) : sbm - 1;
-    uint64_t m = (code << (scale + 1)) >> (R - nMantBits + 1);
-    if (sign) m += 1ull << (nMantBits - 1);
-    return (uint32_t)m;
+    const bool sign = __builtin_signbit(x);
+    const uint32_t code = pac_quant_abs32(sign ? -x : x, nMantBits + 15);
+    uint32_t m = code >> (15 - scale);
+    if (sign) m += 1u << (nMantBits - 1);
+    return m;
 }
 
 // pcmfile.py:89-98 + quantize.py:120-145: +-2|c|/65535, -32768 -> +0.0.

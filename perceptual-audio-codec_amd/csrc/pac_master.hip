@@ -1181,7 +1181,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
             if (act) {
                 extra += bitalloc_lane(cur_s, smr_s, bits_s, nl_s, K.smr + gl * PAC_NB, lrms_bits, bitBudget, extra,
                                        16, lane);
-                // scale factors; the allocation's mantissa and sign bits
+                // scale factors; the allocation's mantissa and sign bits (not
+                // unrolled: 25 band peaks in flight would not fit the 96 VGPRs)
+#pragma unroll 1
                 for (int b = 0; b < PAC_NB; ++b) {
                     const int ba = bits_s[b][lane];
                     const int f = pac_scale_factor(K.bandpeak[gl * PAC_NB + b], ba);
@@ -1216,8 +1218,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                         if (bal[u]) {
                             const int ba = bal[u];
                             m[u] = pac_mantissa(x[u], sfl[u], ba);
-                            ent[u] = hsc + (int64_t)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) *
-                                               PAC_HSC_W;
+                            ent[u] = hsc + (int)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) *
+                                               PAC_HSC_W;              // < 2^19: a 32-bit offset
                         }
                     }
 #pragma unroll

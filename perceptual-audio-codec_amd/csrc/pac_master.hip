@@ -1089,6 +1089,8 @@ __device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)
 #ifndef PAC_TAIL_U
 #define PAC_TAIL_U 8      // lines per lane whose loads are in flight together
 #endif
+#define PAC_BUF_OOB ((int)0xF0000000)    // a raw-buffer offset past any 2 GB range: the load returns 0
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // exclusive prefix of an int across the wave by DPP; *total = the wave's sum
 __device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
@@ -1160,6 +1162,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int64_t t_end = !live ? ck.t0 : (ck.t0 + ck.S < len ? ck.t0 + ck.S : len);
     long extra = live ? st_extra[s] : 0, deposit = live ? st_deposit[s] : 0;
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    // the chunk's coded lines and the Huffman scoring table as raw buffers (2 GB
+    // ranges: PAC_BUF_OOB offsets read 0 without a memory access)
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)K.lines, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc((void*)hsc, 0, 0x7fffffff, 0x00020000);
     for (int64_t t = ck.t0; t < ck.t0 + ck.S; ++t) {   // wave-uniform trip count
         const bool act = t < t_end;
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
@@ -1194,42 +1200,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                     nsign += ba ? nl_s[b] : 0;
                 }
                 // mantissas (stored for the emission / the pack) and the ten
-                // tables' total lengths, PAC_TAIL_U lines at a time (their loads
-                // in flight together)
-                const double* ln = K.lines + gl * PAC_HALFN;
+                // tables' total lengths, PAC_TAIL_U lines at a time, branch-free:
+                // the group's bands from one scalar load, its lanes' bits and
+                // scale factors from LDS, then the lines and the scoring-table
+                // entries by raw buffer loads whose offset is out of range for a
+                // line without bits -- the load returns 0 and touches no memory --
+                // instead of a predicated branch per line (each one a wait on the
+                // band load and the LDS reads before the next line's load)
+                const int64_t lane_off = (int64_t)gl * PAC_HALFN * 8;   // < 2^31: the chunk's line set
                 uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
                 for (int l0 = 0; l0 < lend; l0 += PAC_TAIL_U) {
-                    double x[PAC_TAIL_U];
+                    int bo[PAC_TAIL_U];
+#pragma unroll
+                    for (int u = 0; u < PAC_TAIL_U; ++u) bo[u] = T->band_of_line[l0 + u];   // uniform, one s_load
                     int bal[PAC_TAIL_U], sfl[PAC_TAIL_U];
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; ++u) {
-                        const int l = l0 + u;
-                        const int b = T->band_of_line[l];          // uniform
-                        bal[u] = l < lend ? bits_s[b][lane] : 0;
-                        sfl[u] = sf_s[b][lane];
-                        x[u] = bal[u] ? ln[l] : 0.0;
+                        bal[u] = l0 + u < lend ? bits_s[bo[u]][lane] : 0;
+                        sfl[u] = sf_s[bo[u]][lane];
                     }
+                    double x[PAC_TAIL_U];
+#pragma unroll
+                    for (int u = 0; u < PAC_TAIL_U; ++u)
+                        x[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                            lrs, bal[u] ? (int)(lane_off + (l0 + u) * 8) : PAC_BUF_OOB, 0, 0));
                     uint32_t m[PAC_TAIL_U];
-                    const uint32_t* ent[PAC_TAIL_U];
+                    int eo[PAC_TAIL_U];
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; ++u) {
-                        m[u] = 0u;
-                        ent[u] = hsc;
-                        if (bal[u]) {
-                            const int ba = bal[u];
-                            m[u] = pac_mantissa(x[u], sfl[u], ba);
-                            ent[u] = hsc + (int)(((1 << (ba - 1)) - 2) + (m[u] & ((1u << (ba - 1)) - 1u))) *
-                                               PAC_HSC_W;              // < 2^19: a 32-bit offset
-                        }
+                        const int ba = bal[u];
+                        m[u] = ba ? pac_mantissa(x[u], sfl[u], ba) : 0u;
+                        // < 2^19 entries of 24 B: a 32-bit offset
+                        eo[u] = ba ? ((((1 << (ba - 1)) - 2) + (int)(m[u] & ((1u << (ba - 1)) - 1u))) * PAC_HSC_W) * 4
+                                   : PAC_BUF_OOB;
                     }
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; ++u) {
-                        if (bal[u]) {
-                            const uint2 a = *reinterpret_cast<const uint2*>(ent[u]);
-                            const uint2 b2 = *reinterpret_cast<const uint2*>(ent[u] + 2);
-                            const uint32_t c4 = ent[u][4];
-                            acc[0] += a.x; acc[1] += a.y; acc[2] += b2.x; acc[3] += b2.y; acc[4] += c4;
-                        }
+                        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(hrs, eo[u], 0, 0);
+                        const uint32_t c4 = __builtin_amdgcn_raw_buffer_load_b32(hrs, eo[u] + 16, 0, 0);
+                        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w; acc[4] += c4;
                     }
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; u += 4) {      // four codes per 8-byte store

@@ -8,7 +8,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 set -o pipefail
-T=${MEAS_TAG:-r03}
+T=${MEAS_TAG:-r04}
 run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err || { echo "bench $name failed"; exit 1; }; echo "bench $name: $(grep -o '"value": [0-9.]*' gpurun_out/bench_$name.json)"; }
 run config2 --steps 5 --warmup 1
 run config1 --config 1

@@ -366,6 +366,7 @@ struct pac_ctx {
     bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
     bool side_early = false;               // PAC_SIDE_EARLY=1: side(i+2) beside thr(i+1), spectra double-buffered
     bool tail_early = false;               // PAC_TAIL_EARLY=1: tail(i) right after front(i) (A/B switch)
+    bool mld_skip = true;                  // PAC_MLD_SKIP=0: every MLD row, the pairs in three workgroups per block
     bool front_late = false;               // PAC_FRONT_LATE=1: front(i) on s2 after side(i+1), beside thr(i+1)
                                            // (thresholds double-buffered; measured slower: thr +135 ms for a
                                            // side window -100 ms); default: on s0 beside side(i+1)
@@ -417,6 +418,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_SIDE_EARLY")) c->side_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_TAIL_EARLY")) c->tail_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_FRONT_LATE")) c->front_late = atoi(f) != 0;
+    if (const char* f = getenv("PAC_MLD_SKIP")) c->mld_skip = atoi(f) != 0;
     if (const char* f = getenv("PAC_CHUNK_BLOCKS")) c->chunk_blocks = atoll(f);
     if (const char* f = getenv("PAC_DEBUG_STG_BIAS")) c->stg_bias = std::max<long long>(0, atoll(f)) & ~15ll;
     if (const char* f = getenv("PAC_DEBUG_STG_CAP")) c->stg_cap_max = std::max<long long>(0, atoll(f));
@@ -891,11 +893,15 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     if ((rc = c->m_perm.ensure(n_streams + 1))) return rc;
     HIPCHK(hipMemcpyAsync(c->m_perm.p, perm.data(), n_streams * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     for (Chunk& q : chunks) q.ck.perm = c->m_perm.p;
+    // the MLD skip, pipelined (k_master_thr mode 1): the threshold launch of
+    // chunk i also runs chunk i-1's MLD rows, the front of chunk i-1 follows it;
+    // thresholds and spectra double-, MDCT lines triple-buffered
+    const bool pipe = c->mld_skip && nch == 2 && !c->side_early && !c->front_late && !c->tail_serial;
     if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_msm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
-        (rc = c->m_thr.ensure((c->front_late ? 2 : 1) * cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure((c->side_early ? 2 : 1) * cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
+        (rc = c->m_thr.ensure((c->front_late || pipe ? 2 : 1) * cbmax * 6 * PAC_HALFN)) || (rc = c->m_spec.ensure((c->side_early || pipe ? 2 : 1) * cbmax * 2 * PAC_SPEC_LD)) || (rc = c->m_lines.ensure(3 * cbmax * 2 * PAC_HALFN)) ||
         (rc = c->m_smr.ensure(3 * cbmax * 2 * PAC_NB)) || (rc = c->m_peak.ensure(3 * cbmax * 2 * PAC_NB)))
         return rc;
     pack = pack || dbg_codes;
@@ -938,7 +944,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     // transforms the others)
     const bool side_mdct = c->front_fast && nch == 2 && p->window == PAC_WINDOW_SINE && c->side_fused;
     const bool front_fast = side_mdct && !F.bsf;
-    if (side_mdct && (rc = c->m_mdct.ensure(2 * cbmax * 2 * PAC_HALFN))) return rc;
+    if (side_mdct && (rc = c->m_mdct.ensure((pipe ? 3 : 2) * cbmax * 2 * PAC_HALFN))) return rc;
     if (dbg_codes) {
         if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
             (rc = c->dbg_len.ensure(G * PAC_HALFN)))
@@ -994,12 +1000,12 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     const bool late = c->front_late && !c->side_early && !serial;
     auto bufset = [&](int64_t i) {
         const int64_t k = i % 3;
-        return PacMasterChunkBuf{c->m_thr.p + (late ? (i & 1) * cbmax * 6 * PAC_HALFN : 0),
+        return PacMasterChunkBuf{c->m_thr.p + (late || pipe ? (i & 1) * cbmax * 6 * PAC_HALFN : 0),
                                  c->m_lines.p + k * cbmax * 2 * PAC_HALFN,
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
-                                 c->m_spec.p + (c->side_early ? (i & 1) * cbmax * 2 * PAC_SPEC_LD : 0),
+                                 c->m_spec.p + (c->side_early || pipe ? (i & 1) * cbmax * 2 * PAC_SPEC_LD : 0),
                                  c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
-                                 side_mdct ? c->m_mdct.p + (i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
+                                 side_mdct ? c->m_mdct.p + (pipe ? i % 3 : i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
     };
     // PAC_DEBUG_FLAGS 32: phase clocks of the fused LRMS + spectra kernel, 64: of the front
     // 128: of the thresholds
@@ -1039,19 +1045,32 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         if ((rc = launch_side(1))) return rc;
         spec_ev[1] = event_on(s2);
     }
-    for (int64_t i = 0; i < nck; ++i) {
-        const Chunk& q = chunks[i];
-        const PacMasterChunkBuf K = bufset(i);
-        if (early) spec_ready = spec_ev[i];
-        HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
-        if (i >= 3 && !late) HIPCHK(hipStreamWaitEvent(s0, tail_done[i - 3], 0));   // set k's last reader
+    // iteration i: the thresholds of chunk i (pipe: and chunk i-1's MLD rows),
+    // then the front, tail and emission of chunk f = i (pipe: i - 1)
+    const int64_t d = pipe ? 1 : 0;
+    for (int64_t i = 0; i < nck + d; ++i) {
+        const bool hasA = i < nck;
+        const int64_t f = i - d;
+        if (hasA) {
+            if (early) spec_ready = spec_ev[i];
+            HIPCHK(hipStreamWaitEvent(s0, spec_ready, 0));
+        }
+        if (f >= 3 && !late) HIPCHK(hipStreamWaitEvent(s0, tail_done[f - 3], 0));   // set f % 3's last reader
         if ((rc = mark(0, -1))) return rc;
-        hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(q.B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0, s0,
-                           src_thr, T, K, F, q.ck);
+        if (pipe) {    // mode 1: pairs {0,1}, {2,3} of chunk i, the MLD pair of chunk i - 1
+            const int64_t bA = hasA ? chunks[i].B : 0, bB = i >= 1 ? chunks[i - 1].B : 0;
+            const int64_t ia = hasA ? i : i - 1, ib = i >= 1 ? i - 1 : i;
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(3 * std::max(bA, bB))), dim3(FRONT_NT), 0, s0, src_thr,
+                               T, bufset(ia), F, chunks[ia].ck, bufset(ib), chunks[ib].ck, bA, bB, 1);
+        } else {
+            const PacMasterChunkBuf K = bufset(i);
+            hipLaunchKernelGGL(k_master_thr, dim3((unsigned)(chunks[i].B * (nch == 2 ? 3 : 1))), dim3(FRONT_NT), 0,
+                               s0, src_thr, T, K, F, chunks[i].ck, K, chunks[i].ck, chunks[i].B, (int64_t)0, 0);
+        }
         if ((rc = mark(0, 0))) return rc;
-        if (F.bsf) {   // the short frames' thresholds (the long kernel skips them)
-            hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(q.B * nvar)), dim3(256), 0, s0, src, T, K, F,
-                               q.ck);
+        if (F.bsf && hasA) {   // the short frames' thresholds (the long kernel skips them)
+            hipLaunchKernelGGL(k_master_thr_short, dim3((unsigned)(chunks[i].B * nvar)), dim3(256), 0, s0, src, T,
+                               bufset(i), F, chunks[i].ck);
             if ((rc = mark(0, 6))) return rc;
         }
         const hipEvent_t thr_done = event_on(s0);
@@ -1060,6 +1079,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             if ((rc = launch_side(i + 1))) return rc;
             spec_ready = event_on(s2);
         }
+        if (f < 0) continue;                          // pipe: chunk 0's MLD rows come with chunk 1's launch
+        const Chunk& q = chunks[f];
+        const PacMasterChunkBuf K = bufset(f);
         const hipStream_t sf = late ? s2 : s0;       // the front's stream
         if (late) {
             if (i + 1 >= nck) HIPCHK(hipStreamWaitEvent(s2, thr_done, 0));      // no side(i+1) before it
@@ -1082,7 +1104,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         // i.e. beside the next chunk's thresholds
         HIPCHK(hipStreamWaitEvent(s1, front_done, 0));
         if (i + 1 < nck && !c->tail_early) HIPCHK(hipStreamWaitEvent(s1, early ? spec_ev[i + 1] : spec_ready, 0));
-        if (!pack && i >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[i - 2], 0));   // its codes buffer is free
+        if (!pack && f >= 2) HIPCHK(hipStreamWaitEvent(s1, emit_done[f - 2], 0));   // its codes buffer is free
         if ((rc = mark(1, -1))) return rc;
         // few streams: a wave per stream (the one-lane chain's latency would
         // bound the call), else a lane per stream (fewest VALU instructions)
@@ -1094,15 +1116,15 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                                s1, T, c->hscore.p, K, F, c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
         HIPCHK(hipGetLastError());
         if ((rc = mark(1, 2))) return rc;
-        tail_done[i] = event_on(s1);
+        tail_done[f] = event_on(s1);
         if (!pack) {                                  // this chunk's bitstream, beside the next chunk's tail
-            HIPCHK(hipStreamWaitEvent(s3, tail_done[i], 0));
+            HIPCHK(hipStreamWaitEvent(s3, tail_done[f], 0));
             if ((rc = mark(3, -1))) return rc;
             hipLaunchKernelGGL(k_master_emit, dim3((unsigned)((q.B * nch + WAVE - 1) / WAVE)), dim3(WAVE), 0, s3, T,
                                c->huff, c->hcode.p, K, F, c->blk_off.p, q.ck);
             HIPCHK(hipGetLastError());
             if ((rc = mark(3, 8))) return rc;
-            emit_done[i] = event_on(s3);
+            emit_done[f] = event_on(s3);
         }
     }
     HIPCHK(hipStreamWaitEvent(s0, event_on(s1), 0));

@@ -13,7 +13,9 @@
 //                   calls of getStereoMaskThreshold (psychoac.py:540-562), each
 //                   variant's spectrum derived from FFT(a), FFT(b) (M/S and the
 //                   in-place Hann multiplies in the frequency domain) -> chunk
-//                   thr[j][v][1024], only the rows the variant's bands use
+//                   thr[j][v][1024], only the rows the variant's bands use;
+//                   the MLD pair one launch later, only the rows the M/S
+//                   combination can select (+inf elsewhere)
 //   k_master_front  one workgroup per block: MDCT L/R + overall scale
 //                   (codec.py:237-246), M/S lines, MLD combination and per-band
 //                   SMR selection (psychoac.py:533-682)
@@ -27,7 +29,9 @@
 //                   mantissa codes, sign bits, Huffman codes and LRMS packed
 //                   MSB-first (pacfile.py:288-351) straight to the final offset.
 // The LRMS + spectra of chunk i+1 run beside the front of chunk i, the tail of
-// chunk i beside the thresholds of chunk i+1 (three HIP streams, run_master).
+// chunk i beside the thresholds of chunk i+1 (HIP streams, run_master).  With
+// the MLD skip the threshold launch of chunk i carries chunk i-1's MLD rows
+// and the front of chunk i-1 follows it.
 
 #include "pac_bs.h"
 
@@ -256,16 +260,40 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
 // variant, and the two M/S variants of a pair read the same spectrum
 // neighbourhoods.  Written as two straight-line calls, not a loop: a loop
 // over the variants keeps ~80 more VGPRs live (loop-invariant addresses).
+//
+// mode 1 (the MLD skip, pipelined): the launch for chunk i runs the pairs
+// {0,1}, {2,3} of chunk i (KA, ckA, bA blocks) and the MLD pair {4,5} of
+// chunk i - 1 (KB, ckB, bB blocks), whose {2,3} rows the previous launch
+// wrote.  THR_M = max(BTHR_M, min(BTHR_S, MLD_S)) (psychoac.py:582-591)
+// equals BTHR_M on every line where BTHR_S <= BTHR_M, whatever MLD_S is (and
+// THR_S = BTHR_S where BTHR_M <= BTHR_S): a line needs at most one of MLD_M,
+// MLD_S.  The MLD workgroup reads the block's BTHR_M / BTHR_S rows, computes
+// an MLD row only where one of its lines needs it and stores +inf in the
+// others (min(., +inf) = . : the front's combination then yields BTHR_M /
+// BTHR_S there, as the reference's does).  On correlated stereo BTHR_M >
+// BTHR_S almost everywhere: most blocks need no MLD_S row and skip that
+// variant entirely.  One launch, three kinds of workgroup co-running as in
+// mode 0 (the skip as a separate launch, or as a chain of four variants in
+// one workgroup, measured slower than no skip at all).
 __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const PacTables* __restrict__ T,
-                                                         PacMasterChunkBuf K, PacMasterFields F,
-                                                         PacMasterChunk ck) {
+                                                         PacMasterChunkBuf KA, PacMasterFields F,
+                                                         PacMasterChunk ckA, PacMasterChunkBuf KB,
+                                                         PacMasterChunk ckB, int64_t bA, int64_t bB, int mode) {
     __shared__ double2 buf[1024];                              // spectrum, then masker lists (region A)
     __shared__ __attribute__((aligned(16))) double2 tmp[1024]; // masker lists (region B)
     const int tid = threadIdx.x;
     const int64_t item = xcd_item(blockIdx.x, gridDim.x);
-    const int npair = ck.nch == 2 ? 3 : 1;     // mono master: BTHR_L only
+    // (block, pair) = (item / 3, item % 3); mode 1: pair 2 is the MLD pair of the
+    // previous chunk's block -- interleaved with the others, so that the three
+    // kinds co-run (dispatch follows the item order)
+    const int npair = ckA.nch == 2 ? 3 : 1;     // mono master: BTHR_L only
     const int64_t j = item / npair;            // block within the chunk
-    const int vb = 2 * (int)(item % npair);
+    const int pi = (int)(item % npair);
+    const bool mld = mode == 1 && pi == 2;     // an MLD workgroup of the previous chunk
+    if (j >= (mld ? bB : bA)) return;
+    const PacMasterChunkBuf& K = mld ? KB : KA;
+    const PacMasterChunk& ck = mld ? ckB : ckA;
+    const int vb = 2 * pi;
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, j, &cp)) return;     // uniform per workgroup
     const int64_t gb = cp.gb;
@@ -288,11 +316,40 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     long long* pm = (src.prof && blockIdx.x < PAC_PROF_WG) ? src.prof + (int64_t)blockIdx.x * 4 * PAC_PROF_MARKS
                                                           : nullptr;
     TPROF(0);
+    int rows2 = rows;                          // the second variant's rows
+    if (mld) {
+        // the MLD rows needed: some line with BTHR_M > BTHR_S (MLD_M) -> bits
+        // 0-15, BTHR_S > BTHR_M (MLD_S) -> bits 16-31; each wave a quarter of the rows
+        const int lane = tid & (WAVE - 1), w = tid / WAVE;
+        const double* tm = K.thr + (j * 6 + 2) * PAC_HALFN;
+        uint32_t need = 0u;
+        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
+            if (!((rows >> r) & 1)) continue;
+            const double m = tm[r * WAVE + lane], sv = tm[PAC_HALFN + r * WAVE + lane];
+            if (__ballot(m > sv)) need |= 1u << r;
+            if (__ballot(sv > m)) need |= 1u << (16 + r);
+        }
+        uint32_t* nw = reinterpret_cast<uint32_t*>(tmp);
+        if (lane == 0) nw[w] = need;
+        lds_sync();
+        need = nw[0] | nw[1] | nw[2] | nw[3];
+        lds_sync();                            // read before the lists overwrite tmp
+        const int n4 = rows & ~(int)(need & 0xffffu), n5 = rows & ~(int)(need >> 16);
+        double* o4 = K.thr + (j * 6 + 4) * PAC_HALFN;
+        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
+            if ((n4 >> r) & 1) o4[r * WAVE + lane] = INFINITY;
+            if ((n5 >> r) & 1) o4[PAC_HALFN + r * WAVE + lane] = INFINITY;
+        }
+        rows = __builtin_amdgcn_readfirstlane((int)(need & 0xffffu) & rows);
+        rows2 = __builtin_amdgcn_readfirstlane((int)(need >> 16) & rows2);
+    }
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
     double p[4];
-    grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
-    thr_variant(T, p, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
-    if (ck.nch != 2) return;
+    if (rows) {
+        grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
+        thr_variant(T, p, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
+    }
+    if (ck.nch != 2 || !rows2) return;
     int t2 = tid;                // opaque copy: no per-lane address of the first call is kept live for the second
     asm volatile("" : "+v"(t2));
     // the second variant's spectrum in registers while the other waves finish
@@ -300,7 +357,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     grp_variant_pow_regs<FRONT_NT>(spec, vb + 1, t2, p);
     lds_sync();                                             // the first variant's lists are read
     TPROF(4);
-    thr_variant(T, p, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows, buf, tmp, t2, pm, 5);
+    thr_variant(T, p, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows2, buf, tmp, t2, pm, 5);
     TPROF(8);
 }
 

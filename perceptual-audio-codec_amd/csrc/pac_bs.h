@@ -138,7 +138,7 @@ __device__ __forceinline__ void wave_excl_scan2(double a, double b, double* e0, 
 //                      2^(KL z_l) * prefix sum of 2^(B_m - KL (z_m + 1/2))
 //   upper m < U, loud: 2^(B_m + ku_m (z_l - z_m - 1/2)) directly
 // All terms are positive: the regrouping moves the sum by a few ulp.  Then +
-// threshold in quiet, SPL.  R: the wave's 8 KB of LDS, pw at R + 4096 (2 KB).
+// threshold in quiet, as an intensity.  R: the wave's 8 KB of LDS, pw at R + 4096 (2 KB).
 // out(l, thr) for l < 256 in the 64-line rows whose bit is set in `rows`.
 template <class OUT>
 __device__ __forceinline__ void wave_threshold_short(char* R, const PacTables* __restrict__ T, double drop, int lane,
@@ -250,6 +250,6 @@ __device__ __forceinline__ void wave_threshold_short(char* R, const PacTables* _
             const double t = pac_exp2(__builtin_fma(__dsub_rn(zl, lz[j]) - 0.5, lku[j], lB[j]));
             up += j < Ul ? t : 0.0;
         }
-        out(l, pac_spl((((up + upq) + flat) + lower) + T->tiq_s[l]));
+        out(l, (((up + upq) + flat) + lower) + T->tiq_s[l]);      // the intensity (as wave_masking_row)
     }
 }

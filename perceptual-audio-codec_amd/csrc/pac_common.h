@@ -175,6 +175,34 @@ __device__ __forceinline__ double pac_spl(double I) {
     return s < -30.0 ? -30.0 : s;
 }
 
+// SMR terms without a logarithm per line.  SPL is 96 + 10 log10 of the
+// intensity clamped below at 10^-12.6 (its -30 dB floor), so with thresholds
+// kept as intensities I (k_master_thr, k_origin_front: every threshold lies
+// above the threshold in quiet, far above the floor)
+//   SPL(P) - SPL(I) = 10 log10(max(P, 10^-12.6) / I)
+// and the band maximum of the SMRs (psychoac.py calcStereoSMR / CalcSMRs) is
+// 10 log10 of the band maximum of those ratios: one log10 per band instead of
+// two per line.  Rounding of the same class as the reference's difference of
+// two SPLs (a few ulp of ~100 dB).
+#define PAC_SPL_IMIN 2.51188643150958e-13       // 10^(-126/10): SPL = -30 dB
+// max(P, IMIN) / I for a positive normal I: v_rcp_f64 + two Newton steps
+// (about 1 ulp; the division's IEEE sequence is twice as long)
+__device__ __forceinline__ double pac_spl_ratio(double P, double I) {
+    double r = __builtin_amdgcn_rcp(I);
+    r = __builtin_fma(__builtin_fma(-I, r, 1.0), r, r);
+    r = __builtin_fma(__builtin_fma(-I, r, 1.0), r, r);
+    return (P > PAC_SPL_IMIN ? P : PAC_SPL_IMIN) * r;
+}
+// the SMR of a band maximum q of pac_spl_ratio
+__device__ __forceinline__ double pac_ratio_db(double q) { return 10.0 * pac_log10_pos(q); }
+// MLD thresholds (psychoac.py:582-583, MLD_* = BTHR_*_MLD * mld in dB) as the
+// intensity of that SPL, 10^((mld SPL(I) - 96)/10), so that the M/S
+// combination max(BTHR_M, min(BTHR_S, MLD_S)) (monotone in SPL) runs on
+// intensities
+__device__ __forceinline__ double pac_mld_intensity(double I, double mld) {
+    return pac_exp2((__dmul_rn(pac_spl(I), mld) - 96.0) * 0.33219280948873624);   // log2(10)/10
+}
+
 // QuantizeUniform (quantize.py:40-64) for |a|, R <= 31 bits: the code is below
 // 2^(R-1) <= 2^30, so 32-bit integers carry it (one v_cvt_u32_f64; the
 // float64 -> uint64 conversion is a ~10-instruction sequence)

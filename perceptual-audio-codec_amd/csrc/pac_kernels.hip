@@ -307,19 +307,21 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
     if (nr > 2) thr_l[((rids >> 8) & 15) * WAVE + lane] = tv2;
     if (nr > 3) thr_l[((rids >> 12) & 15) * WAVE + lane] = tv3;
     __syncthreads();
-    // SMR (Origin psychoac.py:281-314) and its band maxima: atomic max on
-    // order-preserving keys of the doubles
+    // SMR (Origin psychoac.py:281-314) and its band maxima: SPL(4 x^2) - SPL(I)
+    // as the intensity ratio (pac_spl_ratio; the thresholds are intensities),
+    // atomic max on the positive doubles' bit patterns, one log10 per band
     unsigned long long* sk = reinterpret_cast<unsigned long long*>(buf + 512);
     if (tid < PAC_NB) sk[tid] = 0ull;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = front_row(i, w) * WAVE + lane;
-        const double smr = pac_spl(4.0 * (x[i] * x[i])) - thr_l[l];
-        if (l < lend) atomicMax(&sk[T->band_of_line[l]], pac_order_key(smr));
+        const double q = pac_spl_ratio(4.0 * (x[i] * x[i]), thr_l[l]);
+        if (l < lend) atomicMax(&sk[T->band_of_line[l]], (unsigned long long)__double_as_longlong(q));
     }
     __syncthreads();
-    if (tid < PAC_NB) W.smr[g * PAC_NB + tid] = T->nlines[tid] ? pac_order_unkey(sk[tid]) : 0.0;
+    if (tid < PAC_NB)
+        W.smr[g * PAC_NB + tid] = T->nlines[tid] ? pac_ratio_db(__longlong_as_double((long long)sk[tid])) : 0.0;
     PROF_MARK(8);
     if (tid == 0) W.overall[g] = (uint8_t)overall;
 }
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(64) void k_debug_threshold(const PacTables* __restr
     const int nm = grp_find_maskers<WAVE>(reinterpret_cast<const double*>(buf), T, no_drop ? 0.0 : 15.0, lane, L);
 #pragma unroll 1
     for (int q = 0; q < 16; ++q)
-        thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = wave_masking_row(L, nm, T, lane, q);
+        thr_out[(int64_t)blockIdx.x * PAC_HALFN + q * WAVE + lane] = pac_spl(wave_masking_row(L, nm, T, lane, q));
     if (lane == 0) npeaks[blockIdx.x] = nm;
 }
 

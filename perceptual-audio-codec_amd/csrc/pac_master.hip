@@ -247,9 +247,10 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
         if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
         const double t = wave_masking_row(L, nm, T, lane, r);
-        // the MLD pair is stored as MLD_M / MLD_S = BTHR_*_MLD * mld (psychoac.py:582-583),
-        // the only form k_master_front reads
-        out[r * WAVE + lane] = v >= 4 ? __dmul_rn(t, T->mld[r * WAVE + lane]) : t;
+        // thresholds as intensities (k_master_front takes the SMRs as ratios,
+        // pac_spl_ratio); the MLD pair as the intensities of MLD_M / MLD_S =
+        // BTHR_*_MLD * mld (psychoac.py:582-583), the only form the front reads
+        out[r * WAVE + lane] = v >= 4 ? pac_mld_intensity(t, T->mld[r * WAVE + lane]) : t;
     }
     TPROF(mk + 2);
 }
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(256) void k_master_thr_short(PacSource src, const P
     wave_spectrum_pow_short(d, T, bufs[k][0], bufs[k][1], pw, lane);
     double* out = K.thr + (j * 6 + v) * PAC_HALFN;
     wave_threshold_short(reinterpret_cast<char*>(bufs[k][0]), T, v >= 4 ? 0.0 : 15.0, lane, rows,
-                         [&](int l, double t) { out[4 * l + k] = v >= 4 ? __dmul_rn(t, T->mld_s[l]) : t; });
+                         [&](int l, double t) { out[4 * l + k] = v >= 4 ? pac_mld_intensity(t, T->mld_s[l]) : t; });
 }
 
 // Block switching: attack flags, one wave per two blocks.  Lane (b, c, s)
@@ -1011,6 +1012,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
         const int b = bl4[i];
         const int ms = ms4[i];
+        // the SMR terms SPL(4 x^2) - THR as intensity ratios (pac_spl_ratio: the
+        // thresholds are intensities, SPL is monotone, so the band maximum of
+        // the ratios gives the band's SMR with one log10; the scale offsets
+        // come off per band)
         double d0, d1;
         if (ms) {
             const double bM = t4[i][0], bS = t4[i][1];
@@ -1019,11 +1024,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
             const double c = bM < mldM ? bM : mldM;
             const double thrS = bS > c ? bS : c;
-            d0 = (pac_spl(4. * (M * M)) - offL) - thrM;
-            d1 = (pac_spl(4. * (S * S)) - offR) - thrS;
+            d0 = pac_spl_ratio(4. * (M * M), thrM);
+            d1 = pac_spl_ratio(4. * (S * S), thrS);
         } else {
-            d0 = (pac_spl(4. * (xl * xl)) - offL) - t4[i][0];
-            d1 = st ? (pac_spl(4. * (xr * xr)) - offR) - t4[i][1] : 0.0;
+            d0 = pac_spl_ratio(4. * (xl * xl), t4[i][0]);
+            d1 = st ? pac_spl_ratio(4. * (xr * xr), t4[i][1]) : 0.0;
         }
         const double v0 = ms ? M : xl, v1 = ms ? S : xr;
         lines[l] = v0;
@@ -1035,7 +1040,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const bool in = l < lend;
         const int lane = tid & (WAVE - 1);
         const int e = in ? min(lane | 15, lane + (T->lower[b] + T->nlines[b] - 1 - l)) : lane;
-        unsigned long long k0 = in ? pac_order_key(d0) : 0ull, k1 = in ? pac_order_key(d1) : 0ull;
+        unsigned long long k0 = in ? (unsigned long long)__double_as_longlong(d0) : 0ull;   // positive: bits order
+        unsigned long long k1 = in ? (unsigned long long)__double_as_longlong(d1) : 0ull;
         unsigned long long k2 = in ? (unsigned long long)__double_as_longlong(fabs(v0)) : 0ull;
         unsigned long long k3 = in ? (unsigned long long)__double_as_longlong(fabs(v1)) : 0ull;
         seg_max_step<1>(k0, k1, k2, k3, lane + 1 <= e);
@@ -1053,8 +1059,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     MPROF(3);
     if (tid < PAC_NB) {
         const bool has = T->nlines[tid] != 0;
-        K.smr[(j * 2 + 0) * PAC_NB + tid] = has ? pac_order_unkey(key[0][tid]) : -96.0;
-        K.smr[(j * 2 + 1) * PAC_NB + tid] = has ? pac_order_unkey(key[1][tid]) : -96.0;
+        // SMR = (SPL(4 x^2) - 6.02 scale) - THR = 10 log10(max ratio) - 6.02 scale
+        // (mono: channel 1 unused, 0 as before)
+        K.smr[(j * 2 + 0) * PAC_NB + tid] =
+            has ? pac_ratio_db(__longlong_as_double((long long)key[0][tid])) - offL : -96.0;
+        K.smr[(j * 2 + 1) * PAC_NB + tid] =
+            has ? (st ? pac_ratio_db(__longlong_as_double((long long)key[1][tid])) - offR : 0.0) : -96.0;
         K.bandpeak[(j * 2 + 0) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[2][tid]) : 0.0;
         K.bandpeak[(j * 2 + 1) * PAC_NB + tid] = has ? __longlong_as_double((long long)key[3][tid]) : 0.0;
     }

@@ -1110,7 +1110,9 @@ __device__ __forceinline__ double mom_group(const MaskerLists& L, const PacTable
 }
 
 // Masking threshold of MDCT row r (lines l = 64 r + lane) by one wave from the
-// masker lists: thr(l) = SPL(I(l) + Intensity(Thresh(f_l))).
+// masker lists, as the intensity I(l) + Intensity(Thresh(f_l)) whose SPL()
+// is the reference's threshold (the SMRs take it as an intensity,
+// pac_spl_ratio).
 __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm, const PacTables* __restrict__ T,
                                                    int lane, int r) {
     const int l = r * WAVE + lane;
@@ -1220,5 +1222,5 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
     RP_ADD(5, nm); RP_ADD(6, L.misc[1]); RP_ADD(7, direct ? 0 : 1); RP_ADD(8, direct ? 0 : D);
     RP_ADD(9, ua - m0); RP_ADD(10, umax - ua); RP_ADD(11, m0); RP_ADD(12, umax);
 #endif
-    return pac_spl((((up + upq) + flat) + lower) + tiq);
+    return (((up + upq) + flat) + lower) + tiq;      // the intensity; SPL() by the caller where needed
 }

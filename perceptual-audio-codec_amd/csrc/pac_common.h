@@ -175,6 +175,12 @@ __device__ __forceinline__ double pac_spl(double I) {
     return s < -30.0 ? -30.0 : s;
 }
 
+// a non-temporal 16-byte store (streamed past the L2's normal allocation)
+__device__ __forceinline__ void nt_store(double2* p, double2 v) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store((d2v){v.x, v.y}, reinterpret_cast<d2v*>(p));
+}
+
 // SMR terms without a logarithm per line.  SPL is 96 + 10 log10 of the
 // intensity clamped below at 10^-12.6 (its -30 dB floor), so with thresholds
 // kept as intensities I (k_master_thr, k_origin_front: every threshold lies

@@ -341,6 +341,7 @@ struct pac_ctx {
     DevBuf<uint8_t> m_lrms, m_overall, m_ba, m_sf, m_tid;
     DevBuf<uint32_t> m_rowm;                // [nblocks] k_master_lrms -> k_master_thr row masks
     DevBuf<uint32_t> m_msm;                 // [nblocks] k_master_lrms -> k_master_front LRMS band masks
+    DevBuf<uint32_t> m_mldm;                // [nblocks] the MLD rows that exist (k_master_lrms, k_master_thr -> front)
     DevBuf<uint16_t> m_codes;               // master: signed mantissa codes per line (tail -> pack; pack path only)
     DevBuf<uint16_t> m_ccodes;              // master: the chunk's codes, tail-internal (emission path)
     DevBuf<uint8_t> m_stg;                  // master: channel-blocks emitted by the tail (staging)
@@ -458,7 +459,7 @@ extern "C" void pac_ctx_destroy(pac_ctx* c) {
     c->bs_att.release(); c->bs_fl.release(); c->dec_bsf.release(); c->m_codes.release();
     if (c->huff) hipFree(c->huff);
     c->m_thr.release(); c->m_lines.release(); c->m_smr.release(); c->m_peak.release(); c->m_spec.release(); c->m_mdct.release();
-    c->m_lrms.release(); c->m_rowm.release(); c->m_msm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
+    c->m_lrms.release(); c->m_rowm.release(); c->m_msm.release(); c->m_mldm.release(); c->m_overall.release(); c->m_ba.release(); c->m_sf.release();
     c->m_tid.release(); c->st_extra.release(); c->st_deposit.release(); c->m_perm.release();
     c->dbg_mant.release(); c->dbg_code.release(); c->dbg_len.release();
     c->hdec_tab.release(); c->dec_data.release(); c->dec_ba.release(); c->dec_sf.release();
@@ -897,7 +898,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     // chunk i also runs chunk i-1's MLD rows, the front of chunk i-1 follows it;
     // thresholds and spectra double-, MDCT lines triple-buffered
     const bool pipe = c->mld_skip && nch == 2 && !c->side_early && !c->front_late && !c->tail_serial;
-    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_msm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
+    if ((rc = c->m_lrms.ensure(nblocks * PAC_NB + 1)) || (rc = c->m_rowm.ensure(nblocks + 1)) || (rc = c->m_msm.ensure(nblocks + 1)) || (rc = c->m_mldm.ensure(nblocks + 1)) || (rc = c->m_overall.ensure(G + 1)) ||
         (rc = c->m_ba.ensure(G * PAC_NB + 1)) || (rc = c->m_sf.ensure(G * PAC_NB + 1)) ||
         (rc = c->m_tid.ensure(G + 1)) || (rc = c->nbytes.ensure(G + 1)) || (rc = c->off.ensure(G + 1)) ||
         (rc = c->tile_sums.ensure((G + SCAN_TILE - 1) / SCAN_TILE + 1)) || (rc = c->grand_total.ensure(1)) ||
@@ -907,7 +908,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     pack = pack || dbg_codes;
     PacMasterFields F{c->m_lrms.p, c->m_overall.p, c->m_ba.p, c->m_sf.p, c->m_tid.p, c->nbytes.p,
                       nullptr, nullptr, nullptr, nullptr, nullptr, c->m_rowm.p, nullptr, nullptr, nullptr, 0,
-                      c->m_msm.p};
+                      c->m_msm.p, c->m_mldm.p};
     if (pack) {
         if ((rc = c->m_codes.ensure(G * PAC_HALFN))) return rc;   // 2 KB per channel-block: tail -> pack
         F.codes = c->m_codes.p;

@@ -85,6 +85,10 @@ struct PacMasterFields {
     unsigned long long* stg_next;   // bump allocator of stg
     int64_t stg_cap;
     uint32_t* msm;       // [nblocks] the LRMS flags as a band mask (bit b: band b M/S), k_master_lrms
+    // [nblocks] the 64-line rows whose MLD_M (bits 0-15) / MLD_S (16-31) thresholds
+    // exist: all ones from k_master_lrms, narrowed by k_master_thr's MLD skip; the
+    // front reads no other MLD row (the others are +inf: min(., +inf) = .)
+    uint32_t* mldm;
 };
 
 // A time slice of a stream group: blocks t0 .. t0+S-1 of the streams
@@ -269,9 +273,9 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
 // equals BTHR_M on every line where BTHR_S <= BTHR_M, whatever MLD_S is (and
 // THR_S = BTHR_S where BTHR_M <= BTHR_S): a line needs at most one of MLD_M,
 // MLD_S.  The MLD workgroup reads the block's BTHR_M / BTHR_S rows, computes
-// an MLD row only where one of its lines needs it and stores +inf in the
-// others (min(., +inf) = . : the front's combination then yields BTHR_M /
-// BTHR_S there, as the reference's does).  On correlated stereo BTHR_M >
+// an MLD row only where one of its lines needs it and records which rows
+// exist (F.mldm); the front takes +inf for the others (min(., +inf) = . : its
+// combination then yields BTHR_M / BTHR_S there, as the reference's does).  On correlated stereo BTHR_M >
 // BTHR_S almost everywhere: most blocks need no MLD_S row and skip that
 // variant entirely.  One launch, three kinds of workgroup co-running as in
 // mode 0 (the skip as a separate launch, or as a chain of four variants in
@@ -335,14 +339,11 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         lds_sync();
         need = nw[0] | nw[1] | nw[2] | nw[3];
         lds_sync();                            // read before the lists overwrite tmp
-        const int n4 = rows & ~(int)(need & 0xffffu), n5 = rows & ~(int)(need >> 16);
-        double* o4 = K.thr + (j * 6 + 4) * PAC_HALFN;
-        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
-            if ((n4 >> r) & 1) o4[r * WAVE + lane] = INFINITY;
-            if ((n5 >> r) & 1) o4[PAC_HALFN + r * WAVE + lane] = INFINITY;
-        }
         rows = __builtin_amdgcn_readfirstlane((int)(need & 0xffffu) & rows);
         rows2 = __builtin_amdgcn_readfirstlane((int)(need >> 16) & rows2);
+        // the rows that exist, for the front (which takes +inf for the others:
+        // no +inf rows are stored or read)
+        if (tid == 0) F.mldm[gb] = (uint32_t)rows | ((uint32_t)rows2 << 16);
     }
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
     double p[4];
@@ -768,6 +769,7 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         if (tid == 0) {
             F.rowm[gb] = (uint32_t)rows;
             F.msm[gb] = msm;
+            F.mldm[gb] = 0xffffffffu;              // every MLD row, unless the MLD skip narrows it
         }
     }
     MPROF(2);
@@ -907,6 +909,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 #pragma unroll
     for (int i = 0; i < 4; ++i) bl4[i] = T->band_of_line[i * 256 + tid];
     const uint32_t msm = st ? F.msm[gb] : 0u;     // mono: all L/R
+    const uint32_t mldm = st ? F.mldm[gb] : 0u;   // the MLD rows that exist (k_master_thr)
     MPROF(0);
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
@@ -972,11 +975,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const double* tp = thr + (ms4[i] ? 2 * PAC_HALFN : 0) + l;
         t4[i][0] = tp[0];
         t4[i][1] = tp[PAC_HALFN];
-        t4[i][2] = t4[i][3] = 0.0;
-        if (ms4[i]) {                  // the MLD pair: M/S lines only (masked lanes fetch nothing)
-            t4[i][2] = tp[2 * PAC_HALFN];
-            t4[i][3] = tp[3 * PAC_HALFN];
-        }
+        // the MLD pair: M/S lines of rows whose MLD rows exist only (masked
+        // lanes fetch nothing); +inf elsewhere, as the reference's min() takes it
+        const int rw = l / WAVE;
+        t4[i][2] = t4[i][3] = INFINITY;
+        if (ms4[i] && ((mldm >> rw) & 1u)) t4[i][2] = tp[2 * PAC_HALFN];
+        if (ms4[i] && ((mldm >> (16 + rw)) & 1u)) t4[i][3] = tp[3 * PAC_HALFN];
     }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     lds_sync();

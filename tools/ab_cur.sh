@@ -1,8 +1,5 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-AB_ARGS="--config 2" bash tools/ab_bench.sh base rag1 || exit 1
-AB_ENV="PAC_CHUNK_BLOCKS=24576" AB_ARGS="--config 2" bash tools/ab_bench.sh base || exit 1
-AB_ENV="PAC_CHUNK_BLOCKS=49152" AB_ARGS="--config 2" bash tools/ab_bench.sh base || exit 1
-AB_ENV="PAC_TAIL_WIDE=1" AB_ARGS="--config 2" bash tools/ab_bench.sh base || exit 1
-AB_ARGS="--config 2" bash tools/ab_bench.sh base rag1 || exit 1
-AB_ENV="PAC_CHUNK_BLOCKS=24576" AB_ARGS="--config 2" bash tools/ab_bench.sh base || exit 1
-AB_ENV="PAC_CHUNK_BLOCKS=49152" AB_ARGS="--config 2" bash tools/ab_bench.sh base || exit 1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_mldm.log 2>&1; tail -2 gpurun_out/t_mldm.log
+AB_ARGS="--config 2" bash tools/ab_bench.sh base mldm base mldm || exit 1
+AB_ARGS="--config 3" bash tools/ab_bench.sh base mldm || exit 1
+AB_ARGS="--config 4" bash tools/ab_bench.sh base mldm || exit 1

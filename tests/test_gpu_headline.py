@@ -169,3 +169,30 @@ def test_front_mdct_paths_agree_on_reference_inputs(ctx):
         c2.close()
     bad = [n for n, a, b in zip(INPUTS, fast, slow) if a != b]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("env", [{"PAC_MLD_SKIP": "0"},          # every MLD row, the pairs in one launch (mode 0)
+                                 {"PAC_TAIL_MODE": "serial"},    # every kernel on one stream, in order
+                                 {"PAC_SIDE_FUSED": "0"}])       # LRMS and spectra as two kernels
+def test_schedules_agree_on_reference_inputs(ctx, env):
+    """The pipelined default (the MLD skip with its row mask, four streams, the
+    fused side kernel) and the alternative schedules give the same bytes on
+    every reference input (the default is pinned to the oracle above)."""
+    paths = [fixture(n) for n in INPUTS]
+    base = pacfile.encode_wav_files(paths, profile=MASTER, context=ctx)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c2 = _lib.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        alt = pacfile.encode_wav_files(paths, profile=MASTER, context=c2)
+    finally:
+        c2.close()
+    bad = [n for n, a, b in zip(INPUTS, base, alt) if a != b]
+    assert not bad, bad

@@ -1,3 +1,2 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-PAC_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu > gpurun_out/r04_rank2.json 2> gpurun_out/r04_rank2.err || { tail -20 gpurun_out/r04_rank2.err; exit 1; }
-tail -1 gpurun_out/r04_rank2.json | cut -c1-400
+timeout -k 10 300 python -u -m pytest tests/test_gpu_headline.py -x -v --timeout 200 --timeout-method thread -k schedules > gpurun_out/t_sched.log 2>&1; tail -6 gpurun_out/t_sched.log

@@ -1,2 +1,3 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_headline.py -x -v --timeout 200 --timeout-method thread -k schedules > gpurun_out/t_sched.log 2>&1; tail -6 gpurun_out/t_sched.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_all.log 2>&1; tail -2 gpurun_out/t_all.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1

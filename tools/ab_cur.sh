@@ -1,3 +1,4 @@
+# scratch A/B driver of the current experiment (gpurun -- 'bash tools/ab_cur.sh'):
+# variants/libpacgpu_<name>.so built by tools/build_variant.py / tools/build_rev.sh
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_all.log 2>&1; tail -2 gpurun_out/t_all.log
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
+AB_ARGS="--config 2" bash tools/ab_bench.sh base eint base eint || exit 1

@@ -65,6 +65,44 @@ def host_cores():
     return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
 
 
+def cgroup_cpus():
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max, v1
+    cfs_quota/period) in CPUs, or None when unlimited / unreadable"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_share():
+    """What the CPU baseline's thread count is measured against: nproc, the
+    affinity set, OMP_NUM_THREADS and the cgroup quota, and why the baseline
+    runs on host_cores() threads"""
+    omp = os.environ.get("OMP_NUM_THREADS")
+    quota = cgroup_cpus()
+    aff = len(os.sched_getaffinity(0))
+    why = []
+    if omp and omp.isdigit() and int(omp) < aff:
+        why.append("OMP_NUM_THREADS=%s is this host's per-job CPU share (the GPU box exports it; its affinity "
+                   "set shows the whole machine's %d CPUs, shared with the other GPUs' jobs)" % (omp, aff))
+    if quota is not None:
+        why.append("cgroup CPU quota %.1f CPUs" % quota)
+    if not why:
+        why.append("every CPU of the affinity set")
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp,
+            "cgroup_quota_cpus": quota, "threads_used": host_cores(), "why": "; ".join(why)}
+
+
 # the reference Python itself, timed in the survey container (BASELINE.md):
 # it cannot run on the GPU box (Python 2 source, /root/reference absent there)
 REF_PYTHON = {"master": {"value": 11.0, "unit": "blocks/s", "cores": 1,
@@ -98,6 +136,9 @@ def parse():
     ap.add_argument("--cpu-blocks", type=int, default=-1,
                     help="encode CPU baseline: blocks per sampled stream (default -1: whole streams, "
                          "~10-15 s on 16 host threads for configs[2])")
+    ap.add_argument("--parity-streams", type=int, default=64,
+                    help="whole streams re-encoded by the CPU oracle and compared with the GPU's bytes, over "
+                         "all ranks (each rank samples ceil(n / world), at least 16, of its own streams)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the CPU baseline (default: the CPUs this process may run on, "
                          "os.sched_getaffinity, capped by OMP_NUM_THREADS when the host sets it -- the "
@@ -155,6 +196,14 @@ class Dist:
 
     def sum(self, v):
         return self._red(v, self.td.ReduceOp.SUM if self.td else None)
+
+    def gather(self, obj):
+        """every rank's obj, in rank order (gloo all_gather_object)"""
+        if not self.td:
+            return [obj]
+        out = [None] * self.world
+        self.td.all_gather_object(out, obj)
+        return out
 
     def close(self):
         if self.td:
@@ -259,6 +308,12 @@ def binding(dom, prof):
                     % (dom, 100 * u)}
 
 
+# kernels launched with dynamic LDS (bytes per workgroup, waves per workgroup):
+# the compiler's resource report shows 0 for them.  k_master_tail: PAC_TAIL_LDS
+# (csrc/pac_master.hip) = 2*25*64*8 + 2*25*64 + 25*4 B, one wave per workgroup
+# (pac_abi.hip run_master launch)
+DYNAMIC_LDS = {"k_master_tail": (2 * 25 * 64 * 8 + 2 * 25 * 64 + 25 * 4, 1)}
+
 # kernels whose occupancy the line reports beside the dominant one
 OCC_KERNELS = ["k_master_lrms_spec", "k_master_front", "k_master_tail", "k_origin_front", "k_master_thr_short"]
 
@@ -296,7 +351,15 @@ def occupancy(kind, kernels):
              "limit_waves_per_simd": r.get("occupancy_waves_per_simd"), "vgprs": r.get("vgprs"),
              "lds_bytes_per_workgroup": r.get("lds_bytes")}
         lds = r.get("lds_bytes") or 0
-        if lds and k not in ("k_master_tail", "k_master_emit"):     # 256-thread workgroups: 4 waves, one per SIMD
+        if k in DYNAMIC_LDS:          # launched with dynamic LDS: the compiler reports 0
+            lds, wg_waves = DYNAMIC_LDS[k]
+            e["lds_bytes_per_workgroup"] = lds
+            e["lds_dynamic"] = True
+            lim = (160 * 1024) // lds * wg_waves / 4.0       # workgroups per CU x waves each / 4 SIMDs
+            e["lds_limit_waves_per_simd"] = lim
+            if e["limit_waves_per_simd"] is not None:
+                e["limit_waves_per_simd"] = min(e["limit_waves_per_simd"], lim)
+        elif lds and k not in ("k_master_tail", "k_master_emit"):     # 256-thread workgroups: 4 waves, one per SIMD
             e["lds_limit_waves_per_simd"] = min(8, (160 * 1024) // lds)
         if m is not None:
             out["source"] = src
@@ -370,16 +433,53 @@ def parity_check(ctx, out_dev, starts, oracle_sections, streams):
     the same streams: channel-blocks compared and how many differ (SURVEY 8(d):
     flip rate)."""
     checked = bad = 0
-    for st, ref in zip(starts, oracle_sections):
+    bad_streams = []
+    for st, ref, sid in zip(starts, oracle_sections, streams):
         if not ref:
             continue
         got = np.empty(len(ref), dtype=np.uint8)
         ctx.to_host(got, out_dev + int(st))
         a, b = channel_blocks(ref), channel_blocks(got.tobytes())
         checked += len(a)
-        bad += sum(1 for x, y in zip(a, b) if x != y) + max(0, len(a) - len(b))
+        nb = sum(1 for x, y in zip(a, b) if x != y) + max(0, len(a) - len(b))
+        bad += nb
+        if nb:
+            bad_streams.append(sid)
     return {"checked_channel_blocks": checked, "mismatching": bad, "streams": streams,
-            "against": "oracle/pac_oracle.c on the CPU-baseline sample (the sampled streams, whole)"}
+            "mismatching_streams": bad_streams}
+
+
+def rank_parity(a, ctx, j, rank, world, threads):
+    """This rank's parity sample: whole streams of its own shard (job j),
+    re-encoded by the CPU oracle on `threads` host threads and compared with
+    the GPU's bytes.  The first `threads` streams (one per thread) are timed as
+    the CPU baseline.  Returns (baseline, parity dict)."""
+    n = min(j.ns, max(16, -(-a.parity_streams // world)))
+    idx = sample_streams(j.ns, n)
+    nt = max(1, min(threads, len(idx)))
+    base, sec0 = cpu_baseline(ctx, j.cpu_samples(idx[:nt]), j.p.sample_rate, a.profile, nt, bs=a.bs,
+                              max_blocks=a.cpu_blocks)
+    sections = list(sec0)
+    if len(idx) > nt:        # the rest of the parity sample, untimed
+        _, more = cpu_baseline(ctx, j.cpu_samples(idx[nt:]), j.p.sample_rate, a.profile, nt, bs=a.bs,
+                               max_blocks=a.cpu_blocks)
+        sections += more
+    par = parity_check(ctx, j.out_dev, [int(j.so[t]) for t in idx], sections, idx)
+    par["rank"] = rank
+    return base, par
+
+
+def merge_parity(per_rank, world):
+    """rank 0's parity entry of the line: the ranks' samples summed"""
+    return {"checked_channel_blocks": sum(p["checked_channel_blocks"] for p in per_rank),
+            "mismatching": sum(p["mismatching"] for p in per_rank),
+            "streams_checked": sum(len(p["streams"]) for p in per_rank),
+            "ranks": [{"rank": p["rank"], "streams": p["streams"], "checked_channel_blocks":
+                       p["checked_channel_blocks"], "mismatching": p["mismatching"],
+                       "mismatching_streams": p["mismatching_streams"]} for p in per_rank],
+            "against": "oracle/pac_oracle.c on the host: every rank re-encodes whole streams of its own shard "
+                       "(stream indices are per rank, into its own job) and compares channel-blocks; %d rank(s)"
+                       % world}
 
 
 class Job:
@@ -700,9 +800,13 @@ def main():
     prof, prof_note = measured_profile("bs" if a.bs else a.profile, dom)   # counters are per workload
     traffic_pb = None
     ref_flop = REF_ALG_FLOP_PER_BLOCK[a.profile]
-    fp64 = {"ref_alg_flop_per_block": ref_flop,
-            "ref_alg_equiv_tflops": ref_flop * blocks / step_s / 1e12 if step_s else None,
-            "peak_tflops": FP64_PEAK_TFLOPS, "profile": prof_note}
+    fp64 = {"peak_tflops": FP64_PEAK_TFLOPS, "profile": prof_note}
+    ref_equiv = {"not_a_roofline": True,
+                 "ref_alg_flop_per_block": ref_flop,
+                 "ref_alg_equiv_tflops": ref_flop * blocks / step_s / 1e12 if step_s else None,
+                 "note": "the reference's direct masking sum priced at ~35 FP64 flop per (masker, line) pair "
+                         "(SURVEY 8(d)) at this line's block rate: what the reference ALGORITHM would need, not "
+                         "flops executed here (the kernels evaluate factored sums; executed flops: fp64)"}
     if prof:
         if "hbm_read_bytes_per_block" in prof:
             traffic_pb = prof["hbm_read_bytes_per_block"] + prof["hbm_write_bytes_per_block"]
@@ -775,6 +879,7 @@ def main():
                    % dist.world, "tail_mode": os.environ.get("PAC_TAIL_MODE", "overlap")},
         "roofline": roofline,
         "fp64": fp64,
+        "ref_alg_equivalent": ref_equiv,
         "kernels_ms": kern_ms,
         "occupancy": occupancy("bs" if a.bs else a.profile, [dom] + [k for k in OCC_KERNELS if k in kern_ms and k != dom]),
         "out_bytes_per_gpu": out_bytes,
@@ -786,16 +891,17 @@ def main():
     else:
         res["config"].update({"sample_rate": a.sample_rate, "streams_per_gpu": a.streams,
                               "blocks_per_stream": a.blocks_per_stream})
-    if dist.rank == 0 and dist.world == 1 and not a.no_cpu:
-        # the CPU sample: the first streams of the (first) job, copied back from HBM
-        j = jobs[0]
-        nt = max(1, min(a.cpu_threads, j.ns))
-        idx = sample_streams(j.ns, nt)
-        samples = j.cpu_samples(idx)
-        starts = [int(j.so[t]) for t in idx]
-        res["cpu_baseline"], sections = cpu_baseline(ctx, samples, j.p.sample_rate, a.profile, nt, bs=a.bs,
-                                                     max_blocks=a.cpu_blocks)
-        res["parity"] = parity_check(ctx, j.out_dev, starts, sections, idx)
+    if not a.no_cpu:
+        # every rank checks whole streams of its own shard against the CPU
+        # oracle (copied back from HBM, after the timed region); rank 0 reports
+        # the sum.  The CPU baseline is rank 0's at N=1 only.
+        base, par = rank_parity(a, ctx, jobs[0], dist.rank, dist.world, a.cpu_threads)
+        per_rank = dist.gather(par)
+        if dist.rank == 0:
+            res["parity"] = merge_parity(per_rank, dist.world)
+            if dist.world == 1:
+                base["cpu_share"] = cpu_share()
+                res["cpu_baseline"] = base
     for j in jobs:
         j.free()
     if dist.rank == 0:

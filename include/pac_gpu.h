@@ -245,7 +245,9 @@ int pac_synth_bursts(pac_ctx *ctx, int16_t *dev_pcm, int64_t n_frames, int64_t p
 int pac_sync(pac_ctx *ctx);
 int pac_set_timing(pac_ctx *ctx, int32_t enable);
 /* Stereo blocks per master-profile chunk (device scratch ~113 KB/block); default 32768,
- * 65536 with block switching (the measured optima on MI355X). */
+ * 65536 with block switching (the measured optima on MI355X).  At most 131071
+ * (PAC_CHUNK_MAX: the tail's 32-bit buffer offsets); larger values, and a larger
+ * PAC_CHUNK_BLOCKS environment value at encode time, give PAC_E_ARG. */
 int pac_set_chunk_blocks(pac_ctx *ctx, int64_t blocks);
 int pac_last_timing(pac_ctx *ctx, pac_timing *out);
 /* Parity probe: calcBTHR (psychoac.py:409-456) of n blocks of 2048 float64

@@ -866,6 +866,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     // block switching) -- measured: configs[2] 6.88 -> 6.97 M blocks/s and configs[3]
     // 6.27 -> 6.59 M against 65536; configs[4] 5.39 M at 65536 against 5.30 M
     const int64_t CB = c->chunk_blocks > 0 ? c->chunk_blocks : p->block_switch ? 65536 : 32768;
+    if (CB > PAC_CHUNK_MAX) return set_err(PAC_E_ARG, "chunk_blocks (PAC_CHUNK_BLOCKS) above PAC_CHUNK_MAX (131071)");
     // chunk geometry: groups [g0, g1) of at most CB streams, each ordered by
     // length (longest first, perm); chunk = blocks t0 .. t0+S-1 of the
     // group's streams still running at t0 (a prefix of that order), S =
@@ -981,9 +982,13 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         HIPCHK(hipEventRecord(e, k == 3 ? s3 : k == 2 ? s2 : (k ? s1 : s0)));
         return PAC_OK;
     };
-    auto event_on = [&](hipStream_t st) -> hipEvent_t {   // a fresh ordering event (no timing)
+    // a fresh ordering event (no timing); a failed record would only show as a
+    // wrong order, so the first failure is kept and the call fails with it
+    hipError_t ev_err = hipSuccess;
+    auto event_on = [&](hipStream_t st) -> hipEvent_t {
         const hipEvent_t e = c->pool_event(nev++);
-        hipEventRecord(e, st);
+        const hipError_t r = hipEventRecord(e, st);
+        if (r != hipSuccess && ev_err == hipSuccess) ev_err = r;
         return e;
     };
     // mono: the LRMS flags are all 0 (L/R coding; the 25 bits are still written)
@@ -1130,6 +1135,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
     }
     HIPCHK(hipStreamWaitEvent(s0, event_on(s1), 0));
     HIPCHK(hipStreamWaitEvent(s0, event_on(s3), 0));
+    HIPCHK(ev_err);
     if (c->dbg & (32 | 64 | 128)) {
         HIPCHK(hipStreamWaitEvent(s0, event_on(s2), 0));
         if ((rc = report_phase_clocks(c, s0, nprof))) return rc;
@@ -1551,6 +1557,7 @@ extern "C" int pac_debug_mdct_dft(pac_ctx* c, int32_t n, const double* data, dou
 
 extern "C" int pac_set_chunk_blocks(pac_ctx* c, int64_t blocks) {
     if (!c || blocks < 1) return set_err(PAC_E_ARG, "bad argument");
+    if (blocks > PAC_CHUNK_MAX) return set_err(PAC_E_ARG, "chunk_blocks above PAC_CHUNK_MAX (131071)");
     c->chunk_blocks = blocks;
     return PAC_OK;
 }

@@ -10,6 +10,7 @@
 #define PAC_NTAB 10       // static Huffman tables, Huffman.py:256-262
 #define PAC_NSYM 32768    // unsigned mantissa symbols (ba <= 16 -> 15 magnitude bits)
 #define PAC_MAXMASK 512   // findpeaks can return at most 511 peaks in 1..1022
+#define PAC_CHUNK_MAX 131071   // largest master chunk (blocks): the tail's 32-bit raw-buffer offsets (pac_master.hip)
 
 // Constant tables, generated on the host in float64 with libm following the
 // reference's numpy expressions (see pac_abi.hip build_tables) and uploaded once

@@ -1165,6 +1165,11 @@ __device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)
 #define PAC_TAIL_U 8      // lines per lane whose loads are in flight together
 #endif
 #define PAC_BUF_OOB ((int)0xF0000000)    // a raw-buffer offset past any 2 GB range: the load returns 0
+// the tail addresses a chunk's coded lines through one raw buffer with 32-bit
+// byte offsets up to 2 * chunk_blocks * PAC_HALFN * 8: run_master refuses
+// chunks of more than PAC_CHUNK_MAX blocks, so no offset wraps
+// into the out-of-range value that would silently read zeros
+static_assert(2LL * PAC_CHUNK_MAX * PAC_HALFN * 8 < 0x7fffffffLL, "tail line offsets exceed the buffer range");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // exclusive prefix of an int across the wave by DPP; *total = the wave's sum

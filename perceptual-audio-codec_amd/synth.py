@@ -45,6 +45,64 @@ def pink_tones_pcm(n_frames, fs=48000, seed=1234, pink_level=0.1):
     return _to_int16(np.stack([L, R], 1) * 32767)
 
 
+MS_EXTREMES = ("dualmono", "antiphase", "rsilent", "lsilent", "lsb", "dcpair", "dcpure", "mixed")
+
+
+def ms_extreme_pcm(kind, n_frames, fs=48000, seed=1234):
+    """Stereo streams at the M/S decision's extremes (codec.py:94-102,
+    psychoac.py:549-591): one of M = (L+R)/2, S = (L-R)/2 or a channel is
+    identically zero, or nearly so.  B is the pink-noise + tones left channel
+    kept within [-32767, 32767] so that -B is exact (no -32768 code).
+
+      dualmono   L = R = B                          S == 0, LRMS = 1 in every non-silent band
+      antiphase  L = B, R = -B                      M == 0
+      rsilent    L = B, R = 0
+      lsilent    L = 0, R = B
+      lsb        L = B, R = B + sparse +-1 LSB      S tiny but not zero
+      dcpair     L = B/2 + 10000, R = B/2 - 10000   S a pure DC offset
+      dcpure     L = 10000, R = -3000               constant channels
+      mixed      24-block segments cycling through the kinds above, plus
+                 digital silence and the decorrelated pink + tones pair
+    """
+    n = int(n_frames)
+    base = pink_tones_pcm(n, fs, seed)
+    B = np.maximum(base[:, 0].astype(np.int32), -32767)
+    z = np.zeros_like(B)
+    if kind == "dualmono":
+        L, R = B, B
+    elif kind == "antiphase":
+        L, R = B, -B
+    elif kind == "rsilent":
+        L, R = B, z
+    elif kind == "lsilent":
+        L, R = z, B
+    elif kind == "lsb":
+        rng = np.random.default_rng(seed + 1)
+        d = rng.integers(-1, 2, n) * (rng.random(n) < 1.0 / 256)
+        L, R = B, np.clip(B + d, -32767, 32767)
+    elif kind == "dcpair":
+        L, R = np.clip(B // 2 + 10000, -32767, 32767), np.clip(B // 2 - 10000, -32767, 32767)
+    elif kind == "dcpure":
+        L, R = z + 10000, z - 3000
+    elif kind == "mixed":
+        L, R = np.empty_like(B), np.empty_like(B)
+        seg = 24 * 1024
+        kinds = MS_EXTREMES[:-1] + ("silence", "pinktones")
+        for k, s0 in enumerate(range(0, n, seg)):
+            kk = kinds[k % len(kinds)]
+            s1 = min(n, s0 + seg)
+            if kk == "silence":
+                L[s0:s1] = R[s0:s1] = 0
+            elif kk == "pinktones":
+                L[s0:s1], R[s0:s1] = base[s0:s1, 0], base[s0:s1, 1]
+            else:
+                p = ms_extreme_pcm(kk, n, fs, seed)
+                L[s0:s1], R[s0:s1] = p[s0:s1, 0], p[s0:s1, 1]
+    else:
+        raise ValueError("unknown M/S extreme %r" % kind)
+    return np.stack([L, R], 1).astype(np.int16)
+
+
 _M64 = (1 << 64) - 1
 
 

@@ -12,7 +12,9 @@ of waves -- and then the wide tail over the long streams' last chunks.  The
 streams are sampled across the batch in the library's length order (the tail
 lane of a stream is its position in that order): the first and last streams,
 the tail-wave boundaries 63/64 and 4 095/4 096, the first and last running
-stream of every chunk, plus a stride.
+stream of every chunk, plus a stride; 24 of the sampled streams carry
+M/S-extreme signals (pac_amd.synth.ms_extreme_pcm: dual-mono, anti-phase, a
+silent channel, +-1 LSB differences, DC pairs) instead of pink noise + tones.
 
 Reference: `codec/codec.py:83-129,222-260`, `codec/Huffman.py:353-371`,
 `codec/pacfile.py:273-366,388-503`.
@@ -26,7 +28,7 @@ import pytest
 from conftest import fixture
 
 import pac_amd  # noqa: F401
-from pac_amd import _lib, pacfile
+from pac_amd import _lib, pacfile, synth
 import pyoracle as P
 
 pytestmark = pytest.mark.gpu
@@ -87,6 +89,15 @@ def test_master_headline_geometry_vs_oracle(ctx):
     out_dev = ctx.alloc(cap)
     try:
         ctx.synth_pink_tones(pcm_dev, nframes, fs, seed=777)
+        # M/S extremes (dual-mono, anti-phase, a silent channel, +-1 LSB, DC
+        # pairs, mixed) over sampled streams of the call, in the one-lane tail
+        # and the wide tail alike: codec.py:94-102, psychoac.py:549-591
+        sample = [int(order[k]) for k in _sample_positions(ns, chunks, 97)]
+        sample = sorted(set(sample) | {0, ns - 1})
+        extreme = {i: synth.MS_EXTREMES[k % len(synth.MS_EXTREMES)]
+                   for k, i in enumerate(sample[::max(1, len(sample) // 24)])}
+        for i, kind in extreme.items():
+            ctx.to_device(pcm_dev + int(fo[i]) * 4, synth.ms_extreme_pcm(kind, int(frames[i]), fs, seed=1000 + i))
         p = _lib.params(fs, 2, MASTER)
         _, so = ctx.encode_streams(p, pcm_dev, fo, out=out_dev, out_capacity=cap, pcm_is_device=True,
                                    out_is_device=True, states=st0)
@@ -99,9 +110,7 @@ def test_master_headline_geometry_vs_oracle(ctx):
                 pos += 4 + int.from_bytes(body[pos:pos + 4].tobytes(), "little")
                 n += 1
             assert pos == end and n == 2 * blocks[i], "stream %d: framing" % i
-        sample = [int(order[k]) for k in _sample_positions(ns, chunks, 97)]
-        sample = sorted(set(sample) | {0, ns - 1})
-        assert len(sample) >= 64
+        assert len(sample) >= 64 and len(extreme) >= 24
         pcms = {}
         for i in sample:
             a = np.empty((int(frames[i]), 2), dtype=np.int16)
@@ -173,7 +182,10 @@ def test_front_mdct_paths_agree_on_reference_inputs(ctx):
 
 @pytest.mark.parametrize("env", [{"PAC_MLD_SKIP": "0"},          # every MLD row, the pairs in one launch (mode 0)
                                  {"PAC_TAIL_MODE": "serial"},    # every kernel on one stream, in order
-                                 {"PAC_SIDE_FUSED": "0"}])       # LRMS and spectra as two kernels
+                                 {"PAC_SIDE_FUSED": "0"},        # LRMS and spectra as two kernels
+                                 {"PAC_FRONT_LATE": "1"},        # front(i) beside thr(i+1), thresholds double-buffered
+                                 {"PAC_SIDE_EARLY": "1"},        # side(i+2) beside thr(i+1), spectra double-buffered
+                                 {"PAC_TAIL_EARLY": "1"}])       # tail(i) right after front(i)
 def test_schedules_agree_on_reference_inputs(ctx, env):
     """The pipelined default (the MLD skip with its row mask, four streams, the
     fused side kernel) and the alternative schedules give the same bytes on

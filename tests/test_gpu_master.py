@@ -81,6 +81,29 @@ def test_chunking_invariance(ctx):
     assert chunked == full
 
 
+def test_chunk_blocks_bound(ctx):
+    """chunks above PAC_CHUNK_MAX (131071 blocks) would wrap the
+    tail's 32-bit buffer offsets into zeros -- refused (pac_set_chunk_blocks
+    and PAC_CHUNK_BLOCKS alike); the bound itself encodes the same bytes."""
+    import ctypes as C
+    fs = 48000
+    streams = [synth.pink_tones_pcm(9 * 1024 + 5, fs, seed=8), synth.white_pcm(6 * 1024, 2, seed=9)]
+    full = pacfile.encode_streams(streams, fs, MASTER, context=ctx)
+    c2 = _lib.Context(0)
+    try:
+        assert ctx.L.pac_set_chunk_blocks(c2.h, C.c_int64(131072)) == _lib.PAC_E_ARG
+        assert ctx.L.pac_set_chunk_blocks(c2.h, C.c_int64(131071)) == 0
+        assert pacfile.encode_streams(streams, fs, MASTER, context=c2) == full
+    finally:
+        c2.close()
+    c3 = _ctx_with_env(PAC_CHUNK_BLOCKS=131072)
+    try:
+        with pytest.raises(_lib.PacError):
+            pacfile.encode_streams(streams, fs, MASTER, context=c3)
+    finally:
+        c3.close()
+
+
 def _ctx_with_env(**env):
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})

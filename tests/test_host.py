@@ -334,6 +334,67 @@ def test_bench_dist_gloo_world2(tmp_path):
     assert r.stdout.strip().splitlines() == ["MAX 2.5 SUM 3.0"]
 
 
+BENCH_PARITY_WORKER = r"""
+import importlib.util, json, sys, types
+import numpy as np
+sys.argv = ["bench.py"]
+sys.path.insert(0, "%s/oracle")
+spec = importlib.util.spec_from_file_location("bench", "%s/bench.py")
+b = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(b)
+import pyoracle as P
+from pac_amd import synth
+d = b.Dist()
+fs, ns = 48000, 20
+# this rank's streams and the "GPU" bytes: the oracle's own encodes laid out
+# back to back in a host buffer standing in for HBM; rank 1 corrupts one byte
+# of its stream 5 (a mismatch the parity sample must see and rank 0 report)
+pcm = [synth.pink_tones_pcm(1024 * (3 + (i %% 3)) + 77 * i, fs, seed=100 * d.rank + i) for i in range(ns)]
+o = P.Oracle(fs, huffman=True)
+secs = [o.encode_data(P.MASTER, x) for x in pcm]
+so = np.zeros(ns + 1, dtype=np.int64)
+so[1:] = np.cumsum([len(x) for x in secs])
+hbm = bytearray(b"".join(secs))
+if d.rank == 1:
+    hbm[int(so[5]) + 9] ^= 0x10
+class Ctx:
+    def to_host(self, arr, addr):
+        arr[:] = np.frombuffer(bytes(hbm[addr:addr + arr.nbytes]), dtype=arr.dtype).reshape(arr.shape)
+job = types.SimpleNamespace(ns=ns, so=so, out_dev=0, p=types.SimpleNamespace(sample_rate=fs),
+                            cpu_samples=lambda idx: [pcm[t] for t in idx])
+a = types.SimpleNamespace(parity_streams=24, profile="master", bs=False, cpu_blocks=-1)
+base, par = b.rank_parity(a, Ctx(), job, d.rank, d.world, 4)
+allp = d.gather(par)
+if d.rank == 0:
+    print(json.dumps(b.merge_parity(allp, d.world)))
+d.close()
+"""
+
+
+def test_bench_parity_every_rank_gloo_world2(tmp_path):
+    """bench.py's N>1 parity: every rank re-encodes whole streams
+    of its own shard with the CPU oracle and compares them with its "GPU"
+    bytes; rank 0's line carries both ranks' sampled streams and the summed
+    mismatches (gloo all_gather_object, world size 2 on the CPU; the GPU
+    bytes are stood in by the oracle's own, with one byte of rank 1's stream 5
+    flipped)."""
+    import json
+    script = tmp_path / "p.py"
+    script.write_text(BENCH_PARITY_WORKER % (ROOT, ROOT))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", "29523",
+                        str(script)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert [x["rank"] for x in line["ranks"]] == [0, 1]
+    assert all(len(x["streams"]) == 16 for x in line["ranks"])      # max(16, ceil(24 / 2)), of 20
+    assert line["streams_checked"] == 32
+    assert line["ranks"][0]["mismatching"] == 0
+    assert line["ranks"][1]["mismatching"] == 1 and line["ranks"][1]["mismatching_streams"] == [5]
+    assert line["mismatching"] == 1
+    assert line["checked_channel_blocks"] == sum(x["checked_channel_blocks"] for x in line["ranks"]) > 32 * 8
+
+
 def _bench_module():
     import importlib.util
     saved = sys.argv

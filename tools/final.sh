@@ -1,19 +1,19 @@
 #!/bin/bash
-# Round-4 final measurement, first half (GPU box via gpurun): the GPU test
+# Final measurement of a round, first half (GPU box via gpurun): the GPU test
 # suite, every workload's bench line (CPU baseline + parity sample) and
-# smoke(), at the current build.  The profiles are tools/r04_prof.sh (a
+# smoke(), at the current build.  The profiles are tools/prof.sh (a
 # second call).  Outputs under gpurun_out/; copied into profiles/ locally.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r04_gputests.log 2>&1 || { echo "gpu tests failed"; tail -20 gpurun_out/r04_gputests.log; exit 1; }
-tail -1 gpurun_out/r04_gputests.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${MEAS_TAG:-r05}_gputests.log 2>&1 || { echo "gpu tests failed"; tail -20 gpurun_out/${MEAS_TAG:-r05}_gputests.log; exit 1; }
+tail -1 gpurun_out/${MEAS_TAG:-r05}_gputests.log
 run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err || { echo "bench $name failed"; tail -5 gpurun_out/bench_$name.err; exit 1; }; echo "bench $name: $(grep -o '"value": [0-9.]*' gpurun_out/bench_$name.json)"; }
 run config2
 run config1 --config 1
 run config3 --config 3
 run config4 --config 4
 run decode --mode decode
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
-tail -1 gpurun_out/r04_smoke.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${MEAS_TAG:-r05}_smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
+tail -1 gpurun_out/${MEAS_TAG:-r05}_smoke.log
 echo FINAL_DONE

@@ -4,11 +4,11 @@
 # PMC passes) of master / origin / block switching at the bench geometry, all
 # at the current build.  Outputs under gpurun_out/; copy what is judged into
 # profiles/.   bash tools/round_measure.sh   (run on the GPU box via gpurun)
-#   MEAS_TAG: profile tag prefix (default r03)
+#   MEAS_TAG: profile tag prefix (default r05)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 set -o pipefail
-T=${MEAS_TAG:-r04}
+T=${MEAS_TAG:-r05}
 run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err || { echo "bench $name failed"; exit 1; }; echo "bench $name: $(grep -o '"value": [0-9.]*' gpurun_out/bench_$name.json)"; }
 run config2 --steps 5 --warmup 1
 run config1 --config 1

@@ -1102,35 +1102,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 // gives one bit to the first band with the largest SMR - 6 bits among the
 // valid ones (np.argmax); the stop test takes max(SMR - (bits - 1) 6) over ALL
 // bands -- the valid ones' maximum is the chosen band's (the map is monotone),
-// the invalid ones' is the running max of their frozen values.  cur[b][lane]
-// = SMR - 6 bits (one rounding, as the reference's expression), -inf once the
-// band is invalid.  Returns the bits left minus extra; bits[b][lane] = the
-// allocation.
-__device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)[WAVE], uint8_t (*bits)[WAVE],
-                                              const int* __restrict__ nl_s, const double* __restrict__ smr_g,
-                                              uint32_t lrms_bits, double bitBudget, long extra, int maxMantBits,
-                                              int lane) {
+// the invalid ones' is the running max of their frozen values.  A band's
+// value is SMR - 6 bits (one rounding, as the reference's expression), -inf
+// once the band is invalid (bit 7 of its bits byte).  Returns the bits left
+// minus extra; bits[b][lane] = the allocation.
+//
+// The argmax is a two-level tournament: the 25 bands in five groups of five
+// consecutive bands, gmax[g] / gidx[g] = the group's first maximum.  A round
+// takes the first maximum of the five group maxima (groups in band order, so
+// the first group holding the maximum, whose first maximum is the global first
+// maximum: np.argmax's tie rule) and, after updating the chosen band,
+// re-evaluates only that band's group: 10 + 10 LDS reads and 8 compare-selects
+// per round instead of 50 reads and a 25-deep compare chain.  The band values
+// are recomputed from (bits, SMR) rather than kept: the tail's LDS must stay
+// within what a CU has left beside four threshold workgroups.
+#define PAC_TT_G 5
+#define PAC_BA_OFF 0x80       // bits byte: the band is no longer valid
+__device__ __forceinline__ double tt_value(double sv, int nb) {
+    return (nb & PAC_BA_OFF) ? -INFINITY : __builtin_fma(-6.0, (double)nb, sv);
+}
+__device__ __forceinline__ void tt_group(const double (*smr)[WAVE], const uint8_t (*bits)[WAVE], double (*gmax)[WAVE],
+                                         uint8_t (*gidx)[WAVE], int g, int lane) {
+    const int b0 = PAC_TT_G * g;
+    double v[PAC_TT_G];
 #pragma unroll
-    for (int b = 0; b < PAC_NB; ++b) {
-        const double v = smr_g[b];
-        smr[b][lane] = v;
-        cur[b][lane] = v;
-        bits[b][lane] = 0;
+    for (int k = 0; k < PAC_TT_G; ++k) v[k] = tt_value(smr[b0 + k][lane], bits[b0 + k][lane]);
+    double best = v[0];
+    int bi = b0;
+#pragma unroll
+    for (int k = 1; k < PAC_TT_G; ++k) {
+        const bool take = v[k] > best;               // strict: the first maximum
+        best = take ? v[k] : best;
+        bi = take ? b0 + k : bi;
+    }
+    gmax[g][lane] = best;
+    gidx[g][lane] = (uint8_t)bi;
+}
+
+__device__ __forceinline__ long bitalloc_lane(double (*smr)[WAVE], uint8_t (*bits)[WAVE], double (*gmax)[WAVE],
+                                              uint8_t (*gidx)[WAVE], const int* __restrict__ nl_s,
+                                              const double* __restrict__ smr_g, uint32_t lrms_bits, double bitBudget,
+                                              long extra, int maxMantBits, int lane) {
+    static_assert(PAC_NB == PAC_TT_G * PAC_TT_G, "five groups of five bands");
+#pragma unroll
+    for (int g = 0; g < PAC_TT_G; ++g) {           // values SMR - 6 * 0 = SMR: the groups from the loads
+        double v[PAC_TT_G];
+#pragma unroll
+        for (int k = 0; k < PAC_TT_G; ++k) {
+            const int b = PAC_TT_G * g + k;
+            v[k] = smr_g[b];
+            smr[b][lane] = v[k];
+            bits[b][lane] = 0;
+        }
+        double best = v[0];
+        int bi = PAC_TT_G * g;
+#pragma unroll
+        for (int k = 1; k < PAC_TT_G; ++k) {
+            const bool take = v[k] > best;
+            best = take ? v[k] : best;
+            bi = take ? PAC_TT_G * g + k : bi;
+        }
+        gmax[g][lane] = best;
+        gidx[g][lane] = (uint8_t)bi;
     }
     long total = (long)(bitBudget + (double)extra);
     double frozen = -INFINITY;
     while (true) {
-        // the maximum, then its first band (the values read twice from LDS:
-        // VALU is what the tail shares with the threshold kernel, and 25 live
-        // doubles would push it past the 96 VGPRs it may use beside it)
-        double best = -INFINITY;
+        double best = gmax[0][lane];
+        int ib = gidx[0][lane];
 #pragma unroll
-        for (int b = 0; b < PAC_NB; ++b) best = vmax_f64(best, cur[b][lane]);
+        for (int g = 1; g < PAC_TT_G; ++g) {
+            const double v = gmax[g][lane];
+            const bool take = v > best;
+            best = take ? v : best;
+            ib = take ? (int)gidx[g][lane] : ib;
+        }
         if (best == -INFINITY) break;                  // no valid band left
-        int ib = 0;
-#pragma unroll
-        for (int b = PAC_NB - 1; b >= 0; --b) ib = cur[b][lane] == best ? b : ib;   // the first maximum
-        const int n = bits[ib][lane], nl = nl_s[ib];
+        const int n = bits[ib][lane], nl = nl_s[ib];   // valid: no PAC_BA_OFF flag
         const double sv = smr[ib][lane];
         const double gall = fmax(__builtin_fma(-6.0, (double)(n - 1), sv), frozen);
         bool drop = gall < (((lrms_bits >> ib) & 1u) ? -5.0 : -15.0);
@@ -1142,21 +1190,19 @@ __device__ __forceinline__ long bitalloc_lane(double (*cur)[WAVE], double (*smr)
         } else {
             drop = true;
         }
-        bits[ib][lane] = (uint8_t)nn;
-        if (drop) {
-            cur[ib][lane] = -INFINITY;
-            frozen = fmax(frozen, __builtin_fma(-6.0, (double)(nn - 1), sv));
-        } else {
-            cur[ib][lane] = __builtin_fma(-6.0, (double)nn, sv);
-        }
+        bits[ib][lane] = (uint8_t)(nn | (drop ? PAC_BA_OFF : 0));
+        if (drop) frozen = fmax(frozen, __builtin_fma(-6.0, (double)(nn - 1), sv));
+        tt_group(smr, bits, gmax, gidx, (ib * 13) >> 6, lane);    // ib / 5 for ib < 25
     }
     int back = 0;                                      // bits[bits == 1] = 0, their lines back
 #pragma unroll
     for (int b = 0; b < PAC_NB; ++b) {
-        if (bits[b][lane] == 1) {
+        int n = bits[b][lane] & ~PAC_BA_OFF;
+        if (n == 1) {
             back += nl_s[b];
-            bits[b][lane] = 0;
+            n = 0;
         }
+        bits[b][lane] = (uint8_t)n;
     }
     return total + back - extra;
 }
@@ -1209,7 +1255,17 @@ struct LaneBits {
 // one-wave workgroups per CU and it would then ignore the 5-waves-per-SIMD
 // register budget (96 VGPRs) that lets a tail wave sit beside 4 threshold
 // waves (104 VGPRs each) on a SIMD.
-#define PAC_TAIL_LDS (2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE + PAC_NB * 4)
+// layout: smr[25][64] double | gmax[5][64] double (after BitAlloc: sf[25][64]
+// u8) | bits[25][64] u8 | gidx[5][64] u8 | nl[25] int -- 17.4 KB.  Measured:
+// 28.9 KB still let a tail workgroup sit beside four threshold workgroups on
+// a CU, 31.8 KB did not (the thresholds +72 ms per 10^7 blocks).
+#define PAC_TAIL_LDS_GMAX (PAC_NB * WAVE * 8)
+#define PAC_TAIL_LDS_BITS (PAC_TAIL_LDS_GMAX + PAC_TT_G * WAVE * 8)
+#define PAC_TAIL_LDS_GIDX (PAC_TAIL_LDS_BITS + PAC_NB * WAVE)
+#define PAC_TAIL_LDS_NL (PAC_TAIL_LDS_GIDX + PAC_TT_G * WAVE)
+#define PAC_TAIL_LDS (PAC_TAIL_LDS_NL + PAC_NB * 4)
+static_assert(PAC_TT_G * WAVE * 8 >= PAC_NB * WAVE, "sf aliases gmax");
+static_assert(PAC_TAIL_LDS <= 28900, "tail LDS beside k_master_thr");
 
 // One lane per stream of the chunk, 64 streams per wave: for the stream's
 // blocks t0 .. t0+S-1 in order -- withdrawBits (Huffman.py:363-371,
@@ -1224,11 +1280,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int64_t* __restrict__ blk_off, PacMasterChunk ck, int64_t* __restrict__ st_extra,
     int64_t* __restrict__ st_deposit, double bitBudget) {
     extern __shared__ __attribute__((aligned(16))) char tail_lds[];
-    double (*cur_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds);
-    double (*smr_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds + PAC_NB * WAVE * 8);
-    uint8_t (*bits_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + 2 * PAC_NB * WAVE * 8);
-    uint8_t (*sf_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + 2 * PAC_NB * WAVE * 8 + PAC_NB * WAVE);
-    int* nl_s = reinterpret_cast<int*>(tail_lds + 2 * PAC_NB * WAVE * 8 + 2 * PAC_NB * WAVE);
+    double (*smr_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds);
+    double (*gmax_s)[WAVE] = reinterpret_cast<double (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_GMAX);
+    uint8_t (*sf_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_GMAX);   // after BitAlloc
+    uint8_t (*bits_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_BITS);
+    uint8_t (*gidx_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_GIDX);
+    int* nl_s = reinterpret_cast<int*>(tail_lds + PAC_TAIL_LDS_NL);
     const int lane = threadIdx.x;
     __builtin_amdgcn_s_setprio(3);    // beside k_master_thr's waves (see thr_variant)
     if (lane < PAC_NB) nl_s[lane] = T->nlines[lane];
@@ -1258,26 +1315,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
             if (deposit > 10) { e = deposit / 100; deposit -= e; }
             else if (deposit < 0) { e = deposit; deposit = 0; }
             extra += e;
-            for (int b = 0; b < PAC_NB; ++b) lrms_bits |= (uint32_t)(F.lrms[gb * PAC_NB + b] & 1) << b;
+            lrms_bits = nch == 2 ? F.msm[gb] : 0u;      // the LRMS flags as one band mask (k_master_lrms)
         }
         for (int ch = 0; ch < nch; ++ch) {
             const int64_t gl = j * 2 + ch, g = gb * nch + ch;
             uint16_t* cs = F.codes ? F.codes + g * PAC_HALFN : K.codes + gl * PAC_HALFN;
             int orig = 0, nsign = 0, best = 0, bestid = 1, nb = 0;
             if (act) {
-                extra += bitalloc_lane(cur_s, smr_s, bits_s, nl_s, K.smr + gl * PAC_NB, lrms_bits, bitBudget, extra,
-                                       16, lane);
-                // scale factors; the allocation's mantissa and sign bits (not
-                // unrolled: 25 band peaks in flight would not fit the 96 VGPRs)
+                extra += bitalloc_lane(smr_s, bits_s, gmax_s, gidx_s, nl_s, K.smr + gl * PAC_NB, lrms_bits,
+                                       bitBudget, extra, 16, lane);
+                // scale factors; the allocation's mantissa and sign bits.  Five
+                // band peaks in flight at a time (25 would not fit the 96 VGPRs; one at a time was 25
+                // dependent memory round trips per channel-block)
 #pragma unroll 1
-                for (int b = 0; b < PAC_NB; ++b) {
-                    const int ba = bits_s[b][lane];
-                    const int f = pac_scale_factor(K.bandpeak[gl * PAC_NB + b], ba);
-                    sf_s[b][lane] = (uint8_t)f;
-                    F.ba[g * PAC_NB + b] = (uint8_t)ba;
-                    F.sf[g * PAC_NB + b] = (uint8_t)f;
-                    orig += ba * nl_s[b];
-                    nsign += ba ? nl_s[b] : 0;
+                for (int b0 = 0; b0 < PAC_NB; b0 += 5) {
+                    double pk[5];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) pk[k] = K.bandpeak[gl * PAC_NB + b0 + k];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) {
+                        const int b = b0 + k;
+                        const int ba = bits_s[b][lane];
+                        const int f = pac_scale_factor(pk[k], ba);
+                        sf_s[b][lane] = (uint8_t)f;
+                        F.ba[g * PAC_NB + b] = (uint8_t)ba;
+                        F.sf[g * PAC_NB + b] = (uint8_t)f;
+                        orig += ba * nl_s[b];
+                        nsign += ba ? nl_s[b] : 0;
+                    }
                 }
                 // mantissas (stored for the emission / the pack) and the ten
                 // tables' total lengths, PAC_TAIL_U lines at a time, branch-free:

@@ -223,6 +223,11 @@ __device__ __forceinline__ void grp_variant_pow_store(const double (&p)[4], doub
             pm[(threadIdx.x / WAVE) * PAC_PROF_MARKS + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
     } while (0)
 // (p: the thread's four bins of the variant's |V[k]|^2, grp_variant_pow_regs)
+// The MLD rows a block needs (bits r: MLD_M, 16 + r: MLD_S), recorded by its
+// M/S workgroup for the MLD workgroup of the next launch in the block's MLD_S
+// row slot: each wave its own word of the row's last 16 bytes, which the MLD
+// workgroup reads before it stores any row
+#define MLD_NEED_AT(mld_s_row) reinterpret_cast<uint32_t*>((mld_s_row) + PAC_HALFN - 2)
 __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double (&p)[4],
                                          double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
                                          int tid, long long* pm, int mk) {
@@ -323,26 +328,14 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     TPROF(0);
     int rows2 = rows;                          // the second variant's rows
     if (mld) {
-        // the MLD rows needed: some line with BTHR_M > BTHR_S (MLD_M) -> bits
-        // 0-15, BTHR_S > BTHR_M (MLD_S) -> bits 16-31; each wave a quarter of the rows
-        const int lane = tid & (WAVE - 1), w = tid / WAVE;
-        const double* tm = K.thr + (j * 6 + 2) * PAC_HALFN;
-        uint32_t need = 0u;
-        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
-            if (!((rows >> r) & 1)) continue;
-            const double m = tm[r * WAVE + lane], sv = tm[PAC_HALFN + r * WAVE + lane];
-            if (__ballot(m > sv)) need |= 1u << r;
-            if (__ballot(sv > m)) need |= 1u << (16 + r);
-        }
-        uint32_t* nw = reinterpret_cast<uint32_t*>(tmp);
-        if (lane == 0) nw[w] = need;
-        lds_sync();
-        need = nw[0] | nw[1] | nw[2] | nw[3];
-        lds_sync();                            // read before the lists overwrite tmp
+        // the MLD rows needed (bits 0-15 MLD_M, 16-31 MLD_S), recorded by the
+        // block's M/S workgroup in the previous launch (its rows still in
+        // registers then): the rows that exist, for the front too (which takes
+        // +inf for the others: no +inf rows are stored or read)
+        const uint32_t* nw = MLD_NEED_AT(K.thr + (j * 6 + 5) * PAC_HALFN);
+        const uint32_t need = nw[0] | nw[1] | nw[2] | nw[3];
         rows = __builtin_amdgcn_readfirstlane((int)(need & 0xffffu) & rows);
         rows2 = __builtin_amdgcn_readfirstlane((int)(need >> 16) & rows2);
-        // the rows that exist, for the front (which takes +inf for the others:
-        // no +inf rows are stored or read)
         if (tid == 0) F.mldm[gb] = (uint32_t)rows | ((uint32_t)rows2 << 16);
     }
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
@@ -359,8 +352,46 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     grp_variant_pow_regs<FRONT_NT>(spec, vb + 1, t2, p);
     lds_sync();                                             // the first variant's lists are read
     TPROF(4);
+    // mode 1, M/S pair: what the MLD-need pass below uses, parked in two free
+    // words of the lists' counters across the variant (kept in registers it
+    // would push the kernel past its SGPRs and 104 VGPRs)
+    int* park = masker_lists(buf, tmp).misc + 2;
+    if (t2 == 0) {
+        const bool rec = mode == 1 && vb == 2;
+        *reinterpret_cast<unsigned long long*>(park) =
+            rec ? reinterpret_cast<unsigned long long>(K.thr + j * 6 * PAC_HALFN) : 0ull;
+        park[2] = rows2;
+    }
     thr_variant(T, p, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows2, buf, tmp, t2, pm, 5);
     TPROF(8);
+    const unsigned long long pbase = *reinterpret_cast<volatile unsigned long long*>(park);
+    if (pbase) {
+        // the MLD rows this block needs: THR_S (psychoac.py:582-591) needs
+        // MLD_M where BTHR_M > BTHR_S, THR_M needs MLD_S where BTHR_S > BTHR_M
+        // -- from the rows this workgroup just stored (its other waves' stores,
+        // complete after the fence + barrier, read past the L1 from the L2:
+        // no HBM re-read of the rows a launch later); each wave a quarter of
+        // the rows
+        // workgroup scope: the stores complete to this XCD's L2 (an agent-scope
+        // fence would write the whole L2 back: measured 2x slower overall)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        lds_sync();
+        const int lane = t2 & (WAVE - 1), w = t2 / WAVE;
+        const int prow = __builtin_amdgcn_readfirstlane(park[2]);
+        double* blk = reinterpret_cast<double*>(pbase);
+        const unsigned long long* tm = reinterpret_cast<const unsigned long long*>(blk + 2 * PAC_HALFN);
+        uint32_t need = 0u;
+        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
+            if (!((prow >> r) & 1)) continue;
+            const double m = __builtin_bit_cast(double, __hip_atomic_load(tm + r * WAVE + lane, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT));
+            const double sv = __builtin_bit_cast(double, __hip_atomic_load(tm + PAC_HALFN + r * WAVE + lane,
+                                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (__ballot(m > sv)) need |= 1u << r;
+            if (__ballot(sv > m)) need |= 1u << (16 + r);
+        }
+        if (lane == 0) MLD_NEED_AT(blk + 5 * PAC_HALFN)[w] = need;
+    }
 }
 
 // Block-switching extension (pac_bs.h): the thresholds of a SHORT frame.  One

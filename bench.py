@@ -310,10 +310,11 @@ def binding(dom, prof):
 
 # kernels launched with dynamic LDS (bytes per workgroup, waves per workgroup):
 # the compiler's resource report shows 0 for them.  k_master_tail: PAC_TAIL_LDS
-# (csrc/pac_master.hip) = 17 380 B: smr, group maxima, bits, group indices, nLines;
-# one wave per workgroup
+# (csrc/pac_master.hip) = 22 500 B: smr, group maxima, bits, group indices, nLines,
+# the line quarters' Huffman sums;
+# four waves per workgroup
 # (pac_abi.hip run_master launch)
-DYNAMIC_LDS = {"k_master_tail": (25 * 64 * 8 + 5 * 64 * 8 + 25 * 64 + 5 * 64 + 25 * 4, 1)}
+DYNAMIC_LDS = {"k_master_tail": (25 * 64 * 8 + 5 * 64 * 8 + 25 * 64 + 5 * 64 + 25 * 4 + 4 * 5 * 64 * 4, 4)}
 
 # kernels whose occupancy the line reports beside the dominant one
 OCC_KERNELS = ["k_master_lrms_spec", "k_master_front", "k_master_tail", "k_origin_front", "k_master_thr_short"]

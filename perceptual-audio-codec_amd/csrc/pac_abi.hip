@@ -1118,7 +1118,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
             hipLaunchKernelGGL(k_master_tail_wide, dim3((unsigned)q.n_s), dim3(WAVE), 0, s1, T, c->hscore.p, K, F,
                                c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
         else
-            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((q.n_s + WAVE - 1) / WAVE)), dim3(WAVE), PAC_TAIL_LDS,
+            hipLaunchKernelGGL(k_master_tail, dim3((unsigned)((q.n_s + WAVE - 1) / WAVE)), dim3(PAC_TAIL_Q * WAVE), PAC_TAIL_LDS,
                                s1, T, c->hscore.p, K, F, c->blk_off.p, q.ck, c->st_extra.p, c->st_deposit.p, budget);
         HIPCHK(hipGetLastError());
         if ((rc = mark(1, 2))) return rc;

@@ -1282,31 +1282,40 @@ struct LaneBits {
 };
 
 // LDS: launched with PAC_TAIL_LDS bytes of dynamic shared memory -- declared
-// statically, its 29 KB would cap the compiler's occupancy estimate at 5
-// one-wave workgroups per CU and it would then ignore the 5-waves-per-SIMD
-// register budget (96 VGPRs) that lets a tail wave sit beside 4 threshold
-// waves (104 VGPRs each) on a SIMD.
+// statically, the compiler's occupancy estimate would become LDS-bound and it
+// would then ignore the 5-waves-per-SIMD register budget (96 VGPRs) that lets
+// a tail wave sit beside 4 threshold waves (104 VGPRs each) on a SIMD.
 // layout: smr[25][64] double | gmax[5][64] double (after BitAlloc: sf[25][64]
-// u8) | bits[25][64] u8 | gidx[5][64] u8 | nl[25] int -- 17.4 KB.  Measured:
-// 28.9 KB still let a tail workgroup sit beside four threshold workgroups on
-// a CU, 31.8 KB did not (the thresholds +72 ms per 10^7 blocks).
+// u8) | bits[25][64] u8 | gidx[5][64] u8 | nl[25] int | the line quarters'
+// Huffman sums acc[4][5][64] u32 -- 22.5 KB.  Measured: 28.9 KB still let a
+// tail workgroup sit beside four threshold workgroups on a CU, 31.8 KB did not
+// (the thresholds +72 ms per 10^7 blocks).
 #define PAC_TAIL_LDS_GMAX (PAC_NB * WAVE * 8)
 #define PAC_TAIL_LDS_BITS (PAC_TAIL_LDS_GMAX + PAC_TT_G * WAVE * 8)
 #define PAC_TAIL_LDS_GIDX (PAC_TAIL_LDS_BITS + PAC_NB * WAVE)
 #define PAC_TAIL_LDS_NL (PAC_TAIL_LDS_GIDX + PAC_TT_G * WAVE)
-#define PAC_TAIL_LDS (PAC_TAIL_LDS_NL + PAC_NB * 4)
+#define PAC_TAIL_LDS_ACC (PAC_TAIL_LDS_NL + PAC_NB * 4)
+#define PAC_TAIL_Q 4           // waves per tail workgroup: line quarters of a channel-block
+#define PAC_TAIL_LDS (PAC_TAIL_LDS_ACC + PAC_TAIL_Q * 5 * WAVE * 4)
 static_assert(PAC_TT_G * WAVE * 8 >= PAC_NB * WAVE, "sf aliases gmax");
 static_assert(PAC_TAIL_LDS <= 28900, "tail LDS beside k_master_thr");
+static_assert(PAC_TAIL_LDS_ACC % 4 == 0, "acc alignment");
 
-// One lane per stream of the chunk, 64 streams per wave: for the stream's
-// blocks t0 .. t0+S-1 in order -- withdrawBits (Huffman.py:363-371,
-// codec.py:229), per channel BitAlloc with the extraBits carry (codec.py:
-// 249-260), scale factors and vMantissa (quantize.py:148-342), StripSignBits
-// + Huffman.encodeData's table choice by total length (Huffman.py:274-309),
-// depositBits (codec.py:111-124) -- and each channel-block's byte count.
-// The signed mantissa codes go to the chunk's K.codes for k_master_emit, or
-// to F.codes for k_master_pack.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_master_tail(
+// 64 streams of the chunk per workgroup of four waves, lane l of every wave
+// serving stream blockIdx * 64 + l: for the stream's blocks t0 .. t0+S-1 in
+// order -- withdrawBits (Huffman.py:363-371, codec.py:229), per channel
+// BitAlloc with the extraBits carry (codec.py:249-260) and the scale factors
+// (quantize.py:148-177) in wave 0, one lane per stream (the reservoir chain,
+// no cross-lane work: the fewest VALU instructions); then vMantissa
+// (quantize.py:315-342), StripSignBits + Huffman.encodeData's ten table
+// lengths (Huffman.py:274-309) over the channel-block's lines, a quarter of
+// them per wave; then in wave 0 the table choice, depositBits
+// (codec.py:111-124) and each channel-block's byte count.  The line quarters
+// cut the chain's longest part -- dependent memory round trips, two per eight
+// lines -- by four with the same instructions (measured alone: 555 ms per
+// 10^7 blocks, 366 of them in the lines).  The signed mantissa codes go to the
+// chunk's K.codes for k_master_emit, or to F.codes for k_master_pack.
+__global__ __launch_bounds__(PAC_TAIL_Q * WAVE) __attribute__((amdgpu_waves_per_eu(5))) void k_master_tail(
     const PacTables* __restrict__ T, const uint32_t* __restrict__ hsc, PacMasterChunkBuf K, PacMasterFields F,
     const int64_t* __restrict__ blk_off, PacMasterChunk ck, int64_t* __restrict__ st_extra,
     int64_t* __restrict__ st_deposit, double bitBudget) {
@@ -1317,10 +1326,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     uint8_t (*bits_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_BITS);
     uint8_t (*gidx_s)[WAVE] = reinterpret_cast<uint8_t (*)[WAVE]>(tail_lds + PAC_TAIL_LDS_GIDX);
     int* nl_s = reinterpret_cast<int*>(tail_lds + PAC_TAIL_LDS_NL);
-    const int lane = threadIdx.x;
+    uint32_t (*acc_s)[5][WAVE] = reinterpret_cast<uint32_t (*)[5][WAVE]>(tail_lds + PAC_TAIL_LDS_ACC);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     __builtin_amdgcn_s_setprio(3);    // beside k_master_thr's waves (see thr_variant)
-    if (lane < PAC_NB) nl_s[lane] = T->nlines[lane];
-    wave_sync();                                       // one wave per workgroup; afterwards lanes touch only their columns
+    if (threadIdx.x < PAC_NB) nl_s[threadIdx.x] = T->nlines[threadIdx.x];
+    lds_sync();
     const int sl = blockIdx.x * WAVE + lane;
     const bool live = sl < ck.n_s;                     // every lane stays for the wave-wide steps
     const int nch = ck.nch;
@@ -1328,19 +1339,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int64_t bb0 = blk_off[s];
     const int64_t len = blk_off[s + 1] - bb0;
     const int64_t t_end = !live ? ck.t0 : (ck.t0 + ck.S < len ? ck.t0 + ck.S : len);
-    long extra = live ? st_extra[s] : 0, deposit = live ? st_deposit[s] : 0;
+    long extra = 0, deposit = 0;                        // the reservoir state: wave 0's lanes
+    if (w == 0 && live) {
+        extra = st_extra[s];
+        deposit = st_deposit[s];
+    }
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    const int q0 = w * (PAC_HALFN / PAC_TAIL_Q);       // this wave's quarter of the lines
+    const int q1 = min(q0 + PAC_HALFN / PAC_TAIL_Q, lend);
     // the chunk's coded lines and the Huffman scoring table as raw buffers (2 GB
     // ranges: PAC_BUF_OOB offsets read 0 without a memory access)
     const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)K.lines, 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc((void*)hsc, 0, 0x7fffffff, 0x00020000);
-    for (int64_t t = ck.t0; t < ck.t0 + ck.S; ++t) {   // wave-uniform trip count
+    for (int64_t t = ck.t0; t < ck.t0 + ck.S; ++t) {   // uniform trip count: every barrier is reached
         const bool act = t < t_end;
         const int64_t j = (int64_t)sl * ck.S + (t - ck.t0);
         const int64_t gb = bb0 + t;
         uint32_t lrms_bits = 0;
         long dep_add = 0;
-        if (act) {
+        if (w == 0 && act) {
             // Huffman.withdrawBits (Huffman.py:363-371), codec.py:229
             long e = 0;
             if (deposit > 10) { e = deposit / 100; deposit -= e; }
@@ -1351,13 +1368,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
         for (int ch = 0; ch < nch; ++ch) {
             const int64_t gl = j * 2 + ch, g = gb * nch + ch;
             uint16_t* cs = F.codes ? F.codes + g * PAC_HALFN : K.codes + gl * PAC_HALFN;
-            int orig = 0, nsign = 0, best = 0, bestid = 1, nb = 0;
-            if (act) {
+            int orig = 0, nsign = 0;
+            if (w == 0 && act) {
                 extra += bitalloc_lane(smr_s, bits_s, gmax_s, gidx_s, nl_s, K.smr + gl * PAC_NB, lrms_bits,
                                        bitBudget, extra, 16, lane);
                 // scale factors; the allocation's mantissa and sign bits.  Five
-                // band peaks in flight at a time (25 would not fit the 96 VGPRs; one at a time was 25
-                // dependent memory round trips per channel-block)
+                // band peaks in flight at a time (25 would not fit the 96
+                // VGPRs; one at a time was 25 dependent memory round trips)
 #pragma unroll 1
                 for (int b0 = 0; b0 < PAC_NB; b0 += 5) {
                     double pk[5];
@@ -1375,17 +1392,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                         nsign += ba ? nl_s[b] : 0;
                     }
                 }
+            }
+            lds_sync();                                // bits and scale factors for every wave
+            uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
+            if (act) {
                 // mantissas (stored for the emission / the pack) and the ten
-                // tables' total lengths, PAC_TAIL_U lines at a time, branch-free:
-                // the group's bands from one scalar load, its lanes' bits and
-                // scale factors from LDS, then the lines and the scoring-table
-                // entries by raw buffer loads whose offset is out of range for a
-                // line without bits -- the load returns 0 and touches no memory --
-                // instead of a predicated branch per line (each one a wait on the
-                // band load and the LDS reads before the next line's load)
+                // tables' total lengths of this wave's quarter, PAC_TAIL_U lines
+                // at a time, branch-free: the group's bands from one scalar
+                // load, its lanes' bits and scale factors from LDS, then the
+                // lines and the scoring-table entries by raw buffer loads whose
+                // offset is out of range for a line without bits -- the load
+                // returns 0 and touches no memory -- instead of a predicated
+                // branch per line
                 const int64_t lane_off = (int64_t)gl * PAC_HALFN * 8;   // < 2^31: the chunk's line set
-                uint32_t acc[5] = {0u, 0u, 0u, 0u, 0u};
-                for (int l0 = 0; l0 < lend; l0 += PAC_TAIL_U) {
+                for (int l0 = q0; l0 < q1; l0 += PAC_TAIL_U) {
                     int bo[PAC_TAIL_U];
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; ++u) bo[u] = T->band_of_line[l0 + u];   // uniform, one s_load
@@ -1418,25 +1438,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                     }
 #pragma unroll
                     for (int u = 0; u < PAC_TAIL_U; u += 4) {      // four codes per 8-byte store
-                        const uint64_t w = (uint64_t)m[u] | ((uint64_t)m[u + 1] << 16) | ((uint64_t)m[u + 2] << 32) |
-                                           ((uint64_t)m[u + 3] << 48);
-                        *reinterpret_cast<uint64_t*>(cs + l0 + u) = w;
+                        const uint64_t wd = (uint64_t)m[u] | ((uint64_t)m[u + 1] << 16) | ((uint64_t)m[u + 2] << 32) |
+                                            ((uint64_t)m[u + 3] << 48);
+                        *reinterpret_cast<uint64_t*>(cs + l0 + u) = wd;
                     }
                 }
+            }
+#pragma unroll
+            for (int k = 0; k < 5; ++k) acc_s[w][k][lane] = acc[k];
+            lds_sync();                                // the quarters' sums; bits / sf read by every wave
+            if (w == 0 && act) {
+                int best = 0, bestid = 1;
+                uint32_t tot[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k)            // 16-bit fields, no carry across: sums < 2^16
+                    tot[k] = (acc_s[0][k][lane] + acc_s[1][k][lane]) + (acc_s[2][k][lane] + acc_s[3][k][lane]);
 #pragma unroll
                 for (int tb = 0; tb < PAC_NTAB; ++tb) {
-                    const int v = (int)((acc[tb >> 1] >> (16 * (tb & 1))) & 0xffffu);
+                    const int v = (int)((tot[tb >> 1] >> (16 * (tb & 1))) & 0xffffu);
                     if (tb == 0 || v < best) { best = v; bestid = tb + 1; }
                 }
                 dep_add += (long)orig - ((long)best + nsign + 4);
-                nb = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
                 F.tid[g] = (uint8_t)bestid;
-                F.nbytes[g] = nb;
+                F.nbytes[g] = 4 + (8 + 8 * PAC_NB + nsign + best + PAC_NB + (F.bsf ? 1 : 0) + 7) / 8;
             }
         }
-        if (act) deposit += dep_add;   // depositBits per channel (codec.py:120)
+        if (w == 0 && act) deposit += dep_add;   // depositBits per channel (codec.py:120)
     }
-    if (live) {
+    if (w == 0 && live) {
         st_extra[s] = extra;
         st_deposit[s] = deposit;
     }

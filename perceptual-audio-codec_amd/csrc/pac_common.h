@@ -207,7 +207,7 @@ __device__ __forceinline__ double pac_ratio_db(double q) { return 10.0 * pac_log
 // combination max(BTHR_M, min(BTHR_S, MLD_S)) (monotone in SPL) runs on
 // intensities
 __device__ __forceinline__ double pac_mld_intensity(double I, double mld) {
-    return pac_exp2((__dmul_rn(pac_spl(I), mld) - 96.0) * 0.33219280948873624);   // log2(10)/10
+    return pac_exp2_v((__dmul_rn(pac_spl(I), mld) - 96.0) * 0.33219280948873624);   // log2(10)/10
 }
 
 // QuantizeUniform (quantize.py:40-64) for |a|, R <= 31 bits: the code is below

@@ -14,6 +14,8 @@ run config1 --config 1
 run config3 --config 3
 run config4 --config 4
 run decode --mode decode
+PAC_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench_rank2.json 2> gpurun_out/bench_rank2.err || { echo "rank-2 rehearsal failed"; tail -5 gpurun_out/bench_rank2.err; exit 1; }
+echo "rank-2 rehearsal: $(grep -o '"value": [0-9.]*' gpurun_out/bench_rank2.json)"
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${MEAS_TAG:-r05}_smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
 tail -1 gpurun_out/${MEAS_TAG:-r05}_smoke.log
 echo FINAL_DONE

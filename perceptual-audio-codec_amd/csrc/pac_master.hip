@@ -228,9 +228,12 @@ __device__ __forceinline__ void grp_variant_pow_store(const double (&p)[4], doub
 // row slot: each wave its own word of the row's last 16 bytes, which the MLD
 // workgroup reads before it stores any row
 #define MLD_NEED_AT(mld_s_row) reinterpret_cast<uint32_t*>((mld_s_row) + PAC_HALFN - 2)
+// PRUNE (an MLD variant in mode 1): rows that wave_masking_row<true> finds not
+// needed are not stored and their bit is cleared in the LDS word *kept
+template <bool PRUNE = false>
 __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, const double (&p)[4],
                                          double* __restrict__ out, int v, int rows, double2* buf, double2* tmp,
-                                         int tid, long long* pm, int mk) {
+                                         int tid, long long* pm, int mk, int* kept = nullptr) {
     const int lane = tid & (WAVE - 1);
     // wave priority: the barrier-bound list building above the barrier-free
     // masking rows, so that a workgroup's waves reach its barriers sooner
@@ -255,13 +258,36 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
         if (k >= 16) break;
         const int r = (int)((PAC_ROW_ORDER >> (4 * k)) & 15);
         if (!((rows >> r) & 1)) continue;                   // no line of the row uses this variant
-        const double t = wave_masking_row(L, nm, T, lane, r);
+        double t;
+        if constexpr (PRUNE) {
+            // the M/S rows this MLD row is min-ed with: BTHR_M, BTHR_S of the
+            // block (stored by its M/S workgroup in the previous launch), below
+            // `out` in the block's six rows
+            const double* bt = out - (v - 2) * PAC_HALFN;
+            const double bm = bt[r * WAVE + lane], bsv = bt[PAC_HALFN + r * WAVE + lane];
+            t = v == 4 ? wave_masking_row<true>(L, nm, T, lane, r, bm, bsv)
+                       : wave_masking_row<true>(L, nm, T, lane, r, bsv, bm);
+            if (t < 0.0) {                                      // uniform
+                if (lane == 0) atomicAnd(kept, ~(1 << (r + (v == 5 ? 16 : 0))));
+                continue;
+            }
+        } else {
+            t = wave_masking_row(L, nm, T, lane, r);
+        }
         // thresholds as intensities (k_master_front takes the SMRs as ratios,
         // pac_spl_ratio); the MLD pair as the intensities of MLD_M / MLD_S =
         // BTHR_*_MLD * mld (psychoac.py:582-583), the only form the front reads
         out[r * WAVE + lane] = v >= 4 ? pac_mld_intensity(t, T->mld[r * WAVE + lane]) : t;
     }
     TPROF(mk + 2);
+}
+
+// the MLD workgroup's surviving rows (kept[0]) to F.mldm at the address
+// parked in kept[2..3], once every wave's pruning is in
+__device__ __forceinline__ void mld_rows_back(int* kept, int tid) {
+    lds_sync();
+    if (tid == 0)
+        *reinterpret_cast<uint32_t*>(*reinterpret_cast<volatile unsigned long long*>(kept + 2)) = (uint32_t)kept[0];
 }
 
 // One workgroup per (block, variant pair) -- {0,1} = L/R, {2,3} = M/S,
@@ -323,8 +349,14 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     rows = __builtin_amdgcn_readfirstlane(rows);
     if (!rows) return;
     const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
+    // phase clocks (PAC_DEBUG_FLAGS 128) only in a -DPAC_THR_PROF build: their
+    // pointer would cost the kernel the SGPRs that keep it at 104 VGPRs
+#ifdef PAC_THR_PROF
     long long* pm = (src.prof && blockIdx.x < PAC_PROF_WG) ? src.prof + (int64_t)blockIdx.x * 4 * PAC_PROF_MARKS
                                                           : nullptr;
+#else
+    long long* pm = nullptr;
+#endif
     TPROF(0);
     int rows2 = rows;                          // the second variant's rows
     if (mld) {
@@ -336,10 +368,35 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         const uint32_t need = nw[0] | nw[1] | nw[2] | nw[3];
         rows = __builtin_amdgcn_readfirstlane((int)(need & 0xffffu) & rows);
         rows2 = __builtin_amdgcn_readfirstlane((int)(need >> 16) & rows2);
-        if (tid == 0) F.mldm[gb] = (uint32_t)rows | ((uint32_t)rows2 << 16);
+        // the rows that exist, for the front: these, less the rows the pruning
+        // below finds not needed -- kept in an LDS word with the mask's
+        // address until the end (in registers they would push the kernel past
+        // its SGPRs), written back after the variants
+        if (tid == 0) {
+            int* park = masker_lists(buf, tmp).misc + 2;
+            park[0] = rows | (rows2 << 16);
+            *reinterpret_cast<unsigned long long*>(park + 2) = reinterpret_cast<unsigned long long>(F.mldm + gb);
+        }
     }
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
     double p[4];
+    int* kept = masker_lists(buf, tmp).misc + 2;            // the MLD workgroup's surviving rows (above)
+    if (mld) {         // the MLD pair (mode 1): both variants pruned, the surviving rows written back
+        double* o4 = K.thr + (j * 6 + 4) * PAC_HALFN;
+        if (rows) {
+            grp_variant_pow_regs<FRONT_NT>(spec, 4, tid, p);
+            thr_variant<true>(T, p, o4, 4, rows, buf, tmp, tid, pm, 1, kept);
+        }
+        if (rows2) {
+            int t2 = tid;
+            asm volatile("" : "+v"(t2));
+            grp_variant_pow_regs<FRONT_NT>(spec, 5, t2, p);
+            lds_sync();                                     // the first variant's lists are read
+            thr_variant<true>(T, p, o4 + PAC_HALFN, 5, rows2, buf, tmp, t2, pm, 5, kept);
+        }
+        mld_rows_back(kept, tid);
+        return;
+    }
     if (rows) {
         grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
         thr_variant(T, p, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);

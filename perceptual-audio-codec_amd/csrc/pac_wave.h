@@ -1113,8 +1113,24 @@ __device__ __forceinline__ double mom_group(const MaskerLists& L, const PacTable
 // masker lists, as the intensity I(l) + Intensity(Thresh(f_l)) whose SPL()
 // is the reference's threshold (the SMRs take it as an intensity,
 // pac_spl_ratio).
+//
+// PRUNE (an MLD variant's row, k_master_thr mode 1): the row is only needed
+// where its MLD threshold could fall below the M/S threshold it is min-ed with
+// (psychoac.py:582-591: THR_S = max(BTHR_S, min(BTHR_M, MLD_M)) and
+// symmetrically), i.e. on lines with ref_hi > ref_lo (hi = BTHR_M, lo = BTHR_S
+// for MLD_M) where MLD < ref_hi.  The flat, lower and quiet-upper zones plus
+// the threshold in quiet are a lower bound of the row's intensity (the loud
+// upper-side terms are positive and added first, and rounding to nearest is
+// monotone), and the MLD intensity is nondecreasing in it; if on every such
+// line the bound's MLD intensity already exceeds ref_hi by a 2^-40 margin
+// (far beyond the polynomials' few-ulp non-monotonicity), min(ref_hi, MLD) is
+// ref_hi whatever the rest of the sum, and the row returns -1 (not needed:
+// the front's +inf gives the same combination).  On the bench signal 12 of
+// the ~14 MLD_M rows of a block end here, before the loud-masker sums.
+#define PAC_PRUNE_MARGIN 1.0000000000009095      // 1 + 2^-40
+template <bool PRUNE = false>
 __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm, const PacTables* __restrict__ T,
-                                                   int lane, int r) {
+                                                   int lane, int r, double ref_hi = 0.0, double ref_lo = 0.0) {
     const int l = r * WAVE + lane;
     const double zl = T->bark_line[l];
     const double zr = T->bark_line[r * WAVE];           // smallest z of the row
@@ -1131,6 +1147,11 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
     const double lower = L.sl[pV] * T->pow_mkl[l];
     const double upq = L.su[pU] * T->pow_kl[l];
     const double tiq = T->tiq[l];
+    if constexpr (PRUNE) {
+        const double lb = ((upq + flat) + lower) + tiq;
+        const bool need = ref_hi > ref_lo && !(pac_mld_intensity(lb, T->mld[l]) > ref_hi * PAC_PRUNE_MARGIN);
+        if (!__ballot(need)) return -1.0;              // uniform: the row is not needed
+    }
     RP_T(t1);
     // loud maskers below the line: loud-list ranks [0, Ul)
     const int Ul = L.lpre[U];

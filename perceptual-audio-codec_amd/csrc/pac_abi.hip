@@ -365,6 +365,7 @@ struct pac_ctx {
     int tail_wide = -1;                    // PAC_TAIL_WIDE: 0 one-lane tail only, 1 wave-per-stream only, auto
     bool side_fused = true;                // PAC_SIDE_FUSED=0: LRMS and spectra as two kernels (A/B switch)
     bool front_fast = true;                // PAC_FRONT_FAST=0: the front computes its own MDCTs (A/B switch)
+    bool side_coded = true;                // PAC_SIDE_CODED=0: the front forms the coded lines (k_master_front<false>)
     bool side_early = false;               // PAC_SIDE_EARLY=1: side(i+2) beside thr(i+1), spectra double-buffered
     bool tail_early = false;               // PAC_TAIL_EARLY=1: tail(i) right after front(i) (A/B switch)
     bool mld_skip = true;                  // PAC_MLD_SKIP=0: every MLD row, the pairs in three workgroups per block
@@ -416,6 +417,7 @@ extern "C" int pac_ctx_create(int device, pac_ctx** out) {
     if (const char* f = getenv("PAC_TAIL_WIDE")) c->tail_wide = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_FUSED")) c->side_fused = atoi(f) != 0;
     if (const char* f = getenv("PAC_FRONT_FAST")) c->front_fast = atoi(f) != 0;
+    if (const char* f = getenv("PAC_SIDE_CODED")) c->side_coded = atoi(f) != 0;
     if (const char* f = getenv("PAC_SIDE_EARLY")) c->side_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_TAIL_EARLY")) c->tail_early = atoi(f) != 0;
     if (const char* f = getenv("PAC_FRONT_LATE")) c->front_late = atoi(f) != 0;
@@ -941,12 +943,16 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         F.bsf = c->bs_fl.p;
     }
     // the MDCT lines from the side kernel's LRMS spectra (mdct_from_dft): sine
-    // window, stereo, no block switching; otherwise the front transforms
-    // (with block switching the plain long frames' lines; k_master_front<false>
-    // transforms the others)
+    // window, stereo.  Without block switching the side kernel forms the coded
+    // lines themselves (k_master_lrms_spec<true>: K.lines, with the overall
+    // scale factors) and k_master_front<true> reads them and stores none
+    // (front_fast); otherwise k_master_front<false> reads the side kernel's
+    // MDCT lines (K.mdct; with block switching those of the plain long
+    // frames) and transforms the others itself
     const bool side_mdct = c->front_fast && nch == 2 && p->window == PAC_WINDOW_SINE && c->side_fused;
-    const bool front_fast = side_mdct && !F.bsf;
-    if (side_mdct && (rc = c->m_mdct.ensure((pipe ? 3 : 2) * cbmax * 2 * PAC_HALFN))) return rc;
+    const bool front_fast = side_mdct && !F.bsf && c->side_coded;
+    const bool side_md = side_mdct && !front_fast;
+    if (side_md && (rc = c->m_mdct.ensure((pipe ? 3 : 2) * cbmax * 2 * PAC_HALFN))) return rc;
     if (dbg_codes) {
         if ((rc = c->dbg_mant.ensure(G * PAC_HALFN)) || (rc = c->dbg_code.ensure(G * PAC_HALFN)) ||
             (rc = c->dbg_len.ensure(G * PAC_HALFN)))
@@ -1011,7 +1017,7 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
                                  c->m_smr.p + k * cbmax * 2 * PAC_NB, c->m_peak.p + k * cbmax * 2 * PAC_NB,
                                  c->m_spec.p + (c->side_early || pipe ? (i & 1) * cbmax * 2 * PAC_SPEC_LD : 0),
                                  c->m_ccodes.p + (i & 1) * cbmax * 2 * PAC_HALFN,
-                                 side_mdct ? c->m_mdct.p + (pipe ? i % 3 : i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
+                                 side_md ? c->m_mdct.p + (pipe ? i % 3 : i & 1) * cbmax * 2 * PAC_HALFN : nullptr};
     };
     // PAC_DEBUG_FLAGS 32: phase clocks of the fused LRMS + spectra kernel, 64: of the front
     // 128: of the thresholds
@@ -1025,13 +1031,23 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         else if (c->dbg & 64) src_front.prof = c->prof.p;
         else src_thr.prof = c->prof.p;
     }
+    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr), spec_ev(nck + 1, nullptr);
     auto launch_side = [&](int64_t i) -> int {         // lrms(i), spec(i) on s2
         int rc2;
         const Chunk& q = chunks[i];
         const PacMasterChunkBuf K = bufset(i);
+        // front_fast: the side kernel writes line set i % 3, whose last reader
+        // was the tail of chunk i - 3 (recorded before this launch in every
+        // schedule; it ran beside an earlier threshold launch)
+        if (front_fast && i >= 3 && tail_done[i - 3]) HIPCHK(hipStreamWaitEvent(s2, tail_done[i - 3], 0));
         if ((rc2 = mark(2, -1))) return rc2;
         if (c->side_fused) {          // timed as the spectra phase (spec_ms), lrms_ms = 0
-            hipLaunchKernelGGL(k_master_lrms_spec, dim3((unsigned)q.B), dim3(256), 0, s2, src_side, T, K, F, q.ck);
+            if (front_fast)
+                hipLaunchKernelGGL(k_master_lrms_spec<true>, dim3((unsigned)q.B), dim3(256), 0, s2, src_side, T, K, F,
+                                   q.ck);
+            else
+                hipLaunchKernelGGL(k_master_lrms_spec<false>, dim3((unsigned)q.B), dim3(256), 0, s2, src_side, T, K, F,
+                                   q.ck);
             HIPCHK(hipGetLastError());
             return mark(2, 7);
         }
@@ -1042,7 +1058,6 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         if ((rc2 = mark(2, 7))) return rc2;
         return PAC_OK;
     };
-    std::vector<hipEvent_t> tail_done(nck, nullptr), emit_done(nck, nullptr), spec_ev(nck + 1, nullptr);
     const bool early = c->side_early && !serial;
     if ((rc = launch_side(0))) return rc;
     hipEvent_t spec_ready = event_on(s2);

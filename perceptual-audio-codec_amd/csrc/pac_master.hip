@@ -732,6 +732,16 @@ __global__ __launch_bounds__(256) void k_debug_mdct_dft(const PacTables* __restr
     }
 }
 
+// CODED (a stereo sine-window call without block switching, whose front reads
+// its lines from here): `mdct` receives the block's final coded lines instead
+// of the MDCT lines -- each channel scaled by 2^(overall scale factor)
+// (codec.py:237-246, the scale from the block maximum of its MDCT lines), and
+// M = (L + R)/2, S = (L - R)/2 of the scaled channels in the bands the LRMS
+// decision codes M/S (psychoac.py:551-555, codec.py:94-102) -- exactly the
+// front's expressions; the overall scale factors go to F.overall.  The lines
+// stay in registers across the decision (the front then stores no lines: 16 KB
+// per block less in the side/front window).
+template <bool CODED>
 __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables* __restrict__ T,
                                            const PacMasterFields& F, const ChunkPos& cp, double2* bufA,
                                            double2* bufB, double* __restrict__ mdct) {
@@ -781,17 +791,31 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
     // are read back from HBM by the next kernels anyway, and streaming them
     // through the L2 evicted the PCM block the spectra stage reads again:
     // configs[2] +1.3 %, same-box A/B)
-    if (mdct) {        // the front's MDCT lines from these spectra; thread 0 owns line 1023
+    double cl[4], cr[4];                           // CODED: the lines until the decision is in
+    double mL = 0.0, mR = 0.0;
+    // the front's MDCT lines from these spectra; thread 0 owns line 1023 (CODED:
+    // after the leaf sums below, so that the lines and the sums are not live
+    // together: the kernel's 5 waves per SIMD need <= 96 VGPRs)
+    auto mdct_lines = [&]() {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = 1023 - 256 * i - tid;
             const double2 a0 = bufA[k], b0 = bufB[k];
             const double2 a1 = k == 1023 ? make_double2(nyA, 0.0) : bufA[k + 1];
             const double2 b1 = k == 1023 ? make_double2(nyB, 0.0) : bufB[k + 1];
-            __builtin_nontemporal_store(mdct_from_dft(a0, a1, T, k), mdct + k);
-            __builtin_nontemporal_store(mdct_from_dft(b0, b1, T, k), mdct + PAC_HALFN + k);
+            const double xl = mdct_from_dft(a0, a1, T, k), xr = mdct_from_dft(b0, b1, T, k);
+            if constexpr (CODED) {
+                cl[i] = xl;
+                cr[i] = xr;
+                mL = fmax(mL, fabs(xl));
+                mR = fmax(mR, fabs(xr));
+            } else {
+                __builtin_nontemporal_store(xl, mdct + k);
+                __builtin_nontemporal_store(xr, mdct + PAC_HALFN + k);
+            }
         }
-    }
+    };
+    if (!CODED && mdct) mdct_lines();
     auto sq = [](double2 z) {   // np.power(z, 2) == z*z (npy_cpow n == 2)
         return make_double2(__dsub_rn(__dmul_rn(z.x, z.x), __dmul_rn(z.y, z.y)),
                             __dadd_rn(__dmul_rn(z.x, z.y), __dmul_rn(z.y, z.x)));
@@ -833,10 +857,22 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             lv1.x = __dadd_rn(lv1.x, sm.x); lv1.y = __dadd_rn(lv1.y, sm.y);
         }
     }
+    if (CODED) mdct_lines();
     lds_sync();                                    // every spectrum read: bufA's start holds the leaves
     double2* leafv0 = bufA;
     double2* leafv1 = bufA + 64;
     if (has && sub == 0) { leafv0[lf] = lv0; leafv1[lf] = lv1; }
+    // CODED: the waves' maxima of |line| (max is order-free: the front's block
+    // maxima exactly) and then the decision's band mask in bufB's start
+    double* wmax = reinterpret_cast<double*>(bufB);
+    if constexpr (CODED) {
+        mL = wave_max(mL);
+        mR = wave_max(mR);
+        if ((tid & (WAVE - 1)) == 0) {
+            wmax[tid / WAVE] = mL;
+            wmax[4 + tid / WAVE] = mR;
+        }
+    }
     lds_sync();
     if (tid < WAVE) {                              // wave 0: the decisions and the rows they select
         int rows = 0, ms = 0;
@@ -858,6 +894,28 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             F.rowm[gb] = (uint32_t)rows;
             F.msm[gb] = msm;
             F.mldm[gb] = 0xffffffffu;              // every MLD row, unless the MLD skip narrows it
+            if (CODED) reinterpret_cast<uint32_t*>(wmax + 8)[0] = msm;
+        }
+    }
+    if constexpr (CODED) {
+        lds_sync();
+        const int oL = pac_scale_factor(fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3])), 5);
+        const int oR = pac_scale_factor(fmax(fmax(wmax[4], wmax[5]), fmax(wmax[6], wmax[7])), 5);
+        const uint32_t msm = reinterpret_cast<const uint32_t*>(wmax + 8)[0];
+        const double gL = (double)(1 << oL), gR = (double)(1 << oR);
+        if (tid == 0) {
+            F.overall[gb * 2] = (uint8_t)oL;
+            F.overall[gb * 2 + 1] = (uint8_t)oR;
+        }
+        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = 1023 - 256 * i - tid;
+            const bool ms = k < lend && ((msm >> T->band_of_line[k]) & 1u);
+            const double xl = __dmul_rn(cl[i], gL), xr = __dmul_rn(cr[i], gR);
+            const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
+            __builtin_nontemporal_store(ms ? M : xl, mdct + k);
+            __builtin_nontemporal_store(ms ? S : xr, mdct + PAC_HALFN + k);
         }
     }
     MPROF(2);
@@ -869,7 +927,7 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB: the L and R spectra, then the leaf sums
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    lrms_block(src, T, F, cp, bufA, bufB, nullptr);
+    lrms_block<false>(src, T, F, cp, bufA, bufB, nullptr);
 }
 
 // One 256-thread workgroup per stereo block: the complex spectra A = FFT(a),
@@ -931,16 +989,25 @@ __global__ __launch_bounds__(256) void k_master_spec(PacSource src, const PacTab
 // Both, one workgroup per block: the LRMS decisions, then the windowed
 // spectra in the same 32 KB (one launch and one workgroup prologue per block
 // on the side stream instead of two).
-__global__ __launch_bounds__(256) void k_master_lrms_spec(PacSource src, const PacTables* __restrict__ T,
+// CODED: the call's front is k_master_front<true>, whose coded lines and
+// overall scale factors this kernel writes (lrms_block<true>: K.lines, F.overall).
+// (5 waves per SIMD, as its LDS allows)
+template <bool CODED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_master_lrms_spec(PacSource src, const PacTables* __restrict__ T,
                                                           PacMasterChunkBuf K, PacMasterFields F, PacMasterChunk ck) {
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    // K.mdct: set by the host only for sine-window stereo calls; the plain long
-    // frames' lines (block switching: the other frames transform in the front)
-    if (ck.nch == 2) {
+    // K.mdct: set by the host only for sine-window stereo calls with block
+    // switching; the plain long frames' lines (the other frames transform in
+    // the front)
+    // (CODED calls are stereo; the nch test is kept in both instantiations: without
+    // it the compiler schedules the CODED kernel into 111 VGPRs, or 17 spills at 96)
+    if (CODED && ck.nch == 2) {
+        lrms_block<true>(src, T, F, cp, bufA, bufB, K.lines + blockIdx.x * 2 * PAC_HALFN);
+    } else if (!CODED && ck.nch == 2) {
         const bool md = K.mdct && !(F.bsf && F.bsf[cp.gb]);
-        lrms_block(src, T, F, cp, bufA, bufB, md ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
+        lrms_block<false>(src, T, F, cp, bufA, bufB, md ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
     }
     lds_sync();                                   // the leaf sums are read before the spectra overwrite them
     spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
@@ -971,8 +1038,11 @@ __device__ __forceinline__ void seg_max_step(unsigned long long& k0, unsigned lo
 // lines, MLD threshold combination, SMR selection and the band maxima (LDS
 // atomic max on order-preserving keys).  Only the thresholds of each band's
 // coding mode are read (k_master_thr computes no others).  FAST: a stereo
-// sine-window call without block switching, whose MDCT lines the side kernel
-// derived from the LRMS spectra (K.mdct): no transform here, 1.5 KB of LDS.
+// sine-window call without block switching, whose coded lines and overall
+// scale factors the side kernel formed from the LRMS spectra
+// (k_master_lrms_spec<true>: K.lines, F.overall): no transform, no scaling and
+// no line stores here, 1.5 KB of LDS.  (The general kernel reads the side
+// kernel's MDCT lines, K.mdct, where it has them.)
 template <bool FAST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_master_front(PacSource src, const PacTables* __restrict__ T,
                                                       PacMasterChunkBuf K, PacMasterFields F,
@@ -1001,12 +1071,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     MPROF(0);
 
     // --- MDCT L and R, overall scale factors (codec.py:237-246) -------------
-    double xl4[4], xr4[4];
-    // the lines come from the side kernel (K.mdct): every block of a FAST call;
-    // with block switching, the plain long frames
+    double xl4[4], xr4[4];   // FAST: the coded lines
+    // the lines come from the side kernel: every block of a FAST call (coded,
+    // K.lines); with block switching, the plain long frames (MDCT, K.mdct)
     const bool from_md = FAST || (K.mdct && st && !fl);
     if (from_md) {
-        const double* md = K.mdct + j * 2 * PAC_HALFN;
+        const double* md = (FAST ? K.lines : K.mdct) + j * 2 * PAC_HALFN;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             xl4[i] = md[i * 256 + tid];
@@ -1072,42 +1142,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
     if (tid < 6 * 32) key[tid / 32][tid % 32] = 0ull;
     lds_sync();
-    double mL = 0.0, mR = 0.0;
+    int oL, oR;
+    if constexpr (FAST) {
+        oL = F.overall[gb * 2];
+        oR = F.overall[gb * 2 + 1];
+    } else {
+        double mL = 0.0, mR = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (!from_md) {
-            xl4[i] = XL[i * 256 + tid];
-            xr4[i] = st ? XR[i * 256 + tid] : 0.0;
+        for (int i = 0; i < 4; ++i) {
+            if (!from_md) {
+                xl4[i] = XL[i * 256 + tid];
+                xr4[i] = st ? XR[i * 256 + tid] : 0.0;
+            }
+            mL = fmax(mL, fabs(xl4[i]));
+            mR = fmax(mR, fabs(xr4[i]));
         }
-        mL = fmax(mL, fabs(xl4[i]));
-        mR = fmax(mR, fabs(xr4[i]));
+        mL = wave_max(mL);                           // one LDS atomic per wave, not per thread
+        mR = wave_max(mR);
+        if ((tid & (WAVE - 1)) == 0) {
+            atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
+            atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
+        }
+        lds_sync();
+        oL = pac_scale_factor(__longlong_as_double((long long)key[4][0]), 5);
+        oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
+        if (tid == 0) {
+            F.overall[gb * ck.nch] = (uint8_t)oL;
+            if (st) F.overall[gb * 2 + 1] = (uint8_t)oR;
+        }
     }
-    mL = wave_max(mL);                           // one LDS atomic per wave, not per thread
-    mR = wave_max(mR);
-    if ((tid & (WAVE - 1)) == 0) {
-        atomicMax(&key[4][0], (unsigned long long)__double_as_longlong(mL));
-        atomicMax(&key[5][0], (unsigned long long)__double_as_longlong(mR));
-    }
-    lds_sync();
-    const int oL = pac_scale_factor(__longlong_as_double((long long)key[4][0]), 5);
-    const int oR = pac_scale_factor(__longlong_as_double((long long)key[5][0]), 5);
     const double gL = (double)(1 << oL), gR = (double)(1 << oR);
     const double offL = 6.02 * oL, offR = 6.02 * oR;
     MPROF(2);
-    if (tid == 0) {
-        F.overall[gb * ck.nch] = (uint8_t)oL;
-        if (st) F.overall[gb * 2 + 1] = (uint8_t)oR;
-    }
 
     // --- per-line SMR terms (psychoac.py:533-597), selection (:662-682) ----
     double* lines = K.lines + j * 2 * PAC_HALFN;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = i * 256 + tid;
-        const double xl = __dmul_rn(xl4[i], gL), xr = __dmul_rn(xr4[i], gR);
-        const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
         const int b = bl4[i];
         const int ms = ms4[i];
+        // the coded lines: M/S of the scaled channels, or the scaled L, R
+        double v0, v1;
+        if constexpr (FAST) {                     // formed by the side kernel (lrms_block<true>)
+            v0 = xl4[i];
+            v1 = xr4[i];
+        } else {
+            const double xl = __dmul_rn(xl4[i], gL), xr = __dmul_rn(xr4[i], gR);
+            const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
+            v0 = ms ? M : xl;
+            v1 = ms ? S : xr;
+        }
         // the SMR terms SPL(4 x^2) - THR as intensity ratios (pac_spl_ratio: the
         // thresholds are intensities, SPL is monotone, so the band maximum of
         // the ratios gives the band's SMR with one log10; the scale offsets
@@ -1120,15 +1205,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             const double thrM = bM > a ? bM : a;           // np.maximum(BTHR_M, .)
             const double c = bM < mldM ? bM : mldM;
             const double thrS = bS > c ? bS : c;
-            d0 = pac_spl_ratio(4. * (M * M), thrM);
-            d1 = pac_spl_ratio(4. * (S * S), thrS);
+            d0 = pac_spl_ratio(4. * (v0 * v0), thrM);
+            d1 = pac_spl_ratio(4. * (v1 * v1), thrS);
         } else {
-            d0 = pac_spl_ratio(4. * (xl * xl), t4[i][0]);
-            d1 = st ? pac_spl_ratio(4. * (xr * xr), t4[i][1]) : 0.0;
+            d0 = pac_spl_ratio(4. * (v0 * v0), t4[i][0]);
+            d1 = st ? pac_spl_ratio(4. * (v1 * v1), t4[i][1]) : 0.0;
         }
-        const double v0 = ms ? M : xl, v1 = ms ? S : xr;
-        lines[l] = v0;
-        lines[PAC_HALFN + l] = v1;
+        if constexpr (!FAST) {
+            lines[l] = v0;
+            lines[PAC_HALFN + l] = v1;
+        }
         // band maxima: each DPP row of 16 lines holds whole band pieces; a
         // segmented max (row_shl DPP, no LDS crossbar) down to each piece's
         // first lane, then one LDS atomic per piece (same-address atomics

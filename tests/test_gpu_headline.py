@@ -185,7 +185,8 @@ def test_front_mdct_paths_agree_on_reference_inputs(ctx):
                                  {"PAC_SIDE_FUSED": "0"},        # LRMS and spectra as two kernels
                                  {"PAC_FRONT_LATE": "1"},        # front(i) beside thr(i+1), thresholds double-buffered
                                  {"PAC_SIDE_EARLY": "1"},        # side(i+2) beside thr(i+1), spectra double-buffered
-                                 {"PAC_TAIL_EARLY": "1"}])       # tail(i) right after front(i)
+                                 {"PAC_TAIL_EARLY": "1"},        # tail(i) right after front(i)
+                                 {"PAC_SIDE_CODED": "0"}])       # coded lines formed by the front, not the side kernel
 def test_schedules_agree_on_reference_inputs(ctx, env):
     """The pipelined default (the MLD skip with its row mask, four streams, the
     fused side kernel) and the alternative schedules give the same bytes on

@@ -462,10 +462,14 @@ def rank_parity(a, ctx, j, rank, world, threads):
     base, sec0 = cpu_baseline(ctx, j.cpu_samples(idx[:nt]), j.p.sample_rate, a.profile, nt, bs=a.bs,
                               max_blocks=a.cpu_blocks)
     sections = list(sec0)
-    if len(idx) > nt:        # the rest of the parity sample, untimed
-        _, more = cpu_baseline(ctx, j.cpu_samples(idx[nt:]), j.p.sample_rate, a.profile, nt, bs=a.bs,
+    rest = idx[nt:]          # the rest of the parity sample, untimed, 4 streams per thread at a time
+    for g0 in range(0, len(rest), 4 * nt):
+        _, more = cpu_baseline(ctx, j.cpu_samples(rest[g0:g0 + 4 * nt]), j.p.sample_rate, a.profile, nt, bs=a.bs,
                                max_blocks=a.cpu_blocks)
         sections += more
+        # progress (a large --parity-streams sample runs for minutes)
+        print("rank %d parity: %d / %d streams re-encoded" % (rank, len(sections), len(idx)), file=sys.stderr,
+              flush=True)
     par = parity_check(ctx, j.out_dev, [int(j.so[t]) for t in idx], sections, idx)
     par["rank"] = rank
     return base, par

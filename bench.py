@@ -157,8 +157,84 @@ def parse():
     return a
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` (N > 1) outside torchrun: start N fresh rank
+    processes of this same script (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1, device = LOCAL_RANK), relay rank 0's stdout (the one
+    JSON line) and return the first non-zero exit status.  This parent never
+    initialises the GPU (the library loads lazily, in the ranks), so starting
+    children is safe; if one rank fails the others are terminated -- they would
+    otherwise wait at the barrier."""
+    import signal
+    import subprocess
+    import threading
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs, out0 = [], []
+
+    def stop(*_):
+        raise SystemExit(143)
+
+    prev = signal.signal(signal.SIGTERM, stop)
+    try:
+        for r in range(a.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                       LOCAL_WORLD_SIZE=str(a.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                          text=True))
+        rd = threading.Thread(target=lambda: out0.extend(procs[0].stdout), daemon=True)
+        rd.start()
+        rc = 0
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                print("bench.py: a rank exited with %d; stopping the others" % rc, file=sys.stderr, flush=True)
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        signal.signal(signal.SIGTERM, prev)
+    rd.join(timeout=10)
+    sys.stdout.write("".join(out0))
+    sys.stdout.flush()
+    return rc or next((p.returncode for p in procs if p.returncode), 0)
+
+
+def make_context(dev, huffman):
+    """The device context of this rank.  PAC_BENCH_MOCK_CONTEXT=<file.py> is a
+    TEST-ONLY hook (tests/bench_mock.py): it replaces the HIP context by the
+    file's Context class so that the rank plumbing (spawn, gloo, parity
+    merge) runs on a CPU-only container; a line made that way says so in
+    "mock_context" and is never a measurement."""
+    mock = os.environ.get("PAC_BENCH_MOCK_CONTEXT")
+    if not mock:
+        return _lib.Context(dev, huffman=huffman)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pac_bench_mock", mock)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.Context(dev, huffman=huffman)
+
+
 class Dist:
-    """Barrier + max over ranks; gloo on CPU when launched under torchrun."""
+    """Barrier + max over ranks; gloo on CPU when launched under torchrun (or
+    by spawn_ranks)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -451,16 +527,26 @@ def parity_check(ctx, out_dev, starts, oracle_sections, streams):
             "mismatching_streams": bad_streams}
 
 
-def rank_parity(a, ctx, j, rank, world, threads):
+def rank_parity(a, ctx, j, rank, world, threads, dist=None):
     """This rank's parity sample: whole streams of its own shard (job j),
     re-encoded by the CPU oracle on `threads` host threads and compared with
     the GPU's bytes.  The first `threads` streams (one per thread) are timed as
-    the CPU baseline.  Returns (baseline, parity dict)."""
+    the CPU baseline; with `dist`, rank 0 times its baseline while the other
+    ranks wait at a barrier, so its host threads do not share the CPUs with
+    their re-encodes.  Returns (baseline, parity dict)."""
     n = min(j.ns, max(16, -(-a.parity_streams // world)))
     idx = sample_streams(j.ns, n)
     nt = max(1, min(threads, len(idx)))
-    base, sec0 = cpu_baseline(ctx, j.cpu_samples(idx[:nt]), j.p.sample_rate, a.profile, nt, bs=a.bs,
-                              max_blocks=a.cpu_blocks)
+
+    def timed():
+        return cpu_baseline(ctx, j.cpu_samples(idx[:nt]), j.p.sample_rate, a.profile, nt, bs=a.bs,
+                            max_blocks=a.cpu_blocks)
+    if rank == 0:
+        base, sec0 = timed()
+    if dist is not None:
+        dist.barrier()
+    if rank != 0:
+        base, sec0 = timed()
     sections = list(sec0)
     rest = idx[nt:]          # the rest of the parity sample, untimed, 4 streams per thread at a time
     for g0 in range(0, len(rest), 4 * nt):
@@ -738,11 +824,19 @@ PHASES["bs"] = PHASES["master"] + [("thr_short_ms", "k_master_thr_short")]
 
 def main():
     a = parse()
+    world = os.environ.get("WORLD_SIZE")
+    if world is None and a.gpus > 1:
+        sys.exit(spawn_ranks(a))            # N fresh rank processes, one per GPU
+    if world is not None and int(world) != a.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%s: launch one rank per GPU with --gpus equal to the number "
+              "of ranks" % (a.gpus, world), file=sys.stderr)
+        sys.exit(2)
     dist = Dist()
     # one GPU per rank (LOCAL_RANK); PAC_BENCH_SHARE_GPU=1 puts every rank on
     # device 0 -- a rehearsal of the multi-rank path on a one-GPU box only
-    dev = 0 if os.environ.get("PAC_BENCH_SHARE_GPU") == "1" else dist.local
-    ctx = _lib.Context(dev, huffman=a.master)
+    share = os.environ.get("PAC_BENCH_SHARE_GPU") == "1"
+    dev = 0 if share else dist.local
+    ctx = make_context(dev, a.master)
     desc, stereo = None, None
     if a.config == 3:
         jobs, desc, stereo = file_jobs(a, ctx, dist.rank, dist.world)
@@ -816,7 +910,7 @@ def main():
     if prof:
         if "hbm_read_bytes_per_block" in prof:
             traffic_pb = prof["hbm_read_bytes_per_block"] + prof["hbm_write_bytes_per_block"]
-        if "fp64_flop_per_block" in prof:
+        if "fp64_flop_per_block" in prof and dom_s > 0:
             tf = prof["fp64_flop_per_block"] * blocks / dom_s / 1e12
             fp64.update({"kernel": dom, "executed_flop_per_block": prof["fp64_flop_per_block"],
                          "executed_tflops": tf, "executed_frac": tf / FP64_PEAK_TFLOPS})
@@ -900,14 +994,22 @@ def main():
     if not a.no_cpu:
         # every rank checks whole streams of its own shard against the CPU
         # oracle (copied back from HBM, after the timed region); rank 0 reports
-        # the sum.  The CPU baseline is rank 0's at N=1 only.
-        base, par = rank_parity(a, ctx, jobs[0], dist.rank, dist.world, a.cpu_threads)
+        # the sum.  The CPU baseline is rank 0's, timed while the other ranks
+        # wait (rank_parity), on rank 0's own host-core share.
+        base, par = rank_parity(a, ctx, jobs[0], dist.rank, dist.world, a.cpu_threads,
+                                dist=dist if dist.world > 1 else None)
         per_rank = dist.gather(par)
         if dist.rank == 0:
             res["parity"] = merge_parity(per_rank, dist.world)
-            if dist.world == 1:
-                base["cpu_share"] = cpu_share()
-                res["cpu_baseline"] = base
+            base["cpu_share"] = cpu_share()
+            if dist.world > 1:
+                base["timed_on"] = ("rank 0 of %d, alone (the other ranks wait at a barrier); cores = rank 0's "
+                                    "host threads" % dist.world)
+            res["cpu_baseline"] = base
+    if os.environ.get("PAC_BENCH_MOCK_CONTEXT"):
+        res["mock_context"] = "TEST ONLY (%s): no GPU ran, not a measurement" % os.environ["PAC_BENCH_MOCK_CONTEXT"]
+    if share and dist.world > 1:
+        res["config"]["shared_gpu"] = "PAC_BENCH_SHARE_GPU=1: all %d ranks on device 0 (rehearsal)" % dist.world
     for j in jobs:
         j.free()
     if dist.rank == 0:

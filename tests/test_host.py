@@ -433,3 +433,53 @@ def test_bench_chunk_geometry_mirror(monkeypatch):
     assert b.master_launches([1000] * 12500, 65536) == 200       # S = 5
     # ragged: 10, 4, 1 blocks in chunks of 4: S = 1 (3 running), 2, 2 (2 running), 4, 1 (one left)
     assert b.master_launches([10, 4, 1], 4) == 5
+
+
+def _bench_env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(kw)
+    return env
+
+
+def test_bench_gpus2_spawns_ranks():
+    """`bench.py --gpus 2` without torchrun: the parent starts two
+    rank processes (gloo), relays rank 0's one JSON line with n_gpus 2, both
+    ranks' parity samples and a cpu_baseline.  The HIP context is replaced by
+    the CPU stand-in tests/bench_mock.py (the oracle's bytes; rank 1's first
+    stream has one byte flipped, which the merged parity must report)."""
+    import json
+    env = _bench_env(PAC_BENCH_MOCK_CONTEXT=os.path.join(ROOT, "tests", "bench_mock.py"), PAC_MOCK_CORRUPT_RANK="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
+                        "1", "--streams", "3", "--blocks-per-stream", "4", "--cpu-threads", "2"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and "mock_context" in line
+    assert line["config"]["global_blocks"] == 2 * line["config"]["blocks_per_gpu"] == 2 * 3 * 4
+    par = line["parity"]
+    assert [x["rank"] for x in par["ranks"]] == [0, 1]
+    assert par["ranks"][0]["mismatching"] == 0
+    assert par["ranks"][1]["mismatching"] == 1 and par["ranks"][1]["mismatching_streams"] == [0]
+    assert par["checked_channel_blocks"] == 2 * 3 * 4 * 2
+    base = line["cpu_baseline"]
+    assert base["kind"] == "port" and base["cores"] == 2 and "rank 0 of 2" in base["timed_on"]
+
+
+def test_bench_gpus_mismatch_refused():
+    """under a launcher, --gpus N must equal WORLD_SIZE (no silent 1-GPU run)"""
+    env = _bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_spawned_rank_failure_is_fatal():
+    """a rank that fails makes `bench.py --gpus 2` exit non-zero with no line"""
+    env = _bench_env(PAC_BENCH_MOCK_CONTEXT=os.path.join(ROOT, "tests", "no_such_mock.py"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--streams", "2", "--blocks-per-stream", "3"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode != 0 and r.stdout.strip() == ""

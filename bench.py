@@ -384,13 +384,33 @@ def binding(dom, prof):
                     % (dom, 100 * u)}
 
 
+def csrc_defines(names, files=("pac_wave.h", "pac_common.h", "pac_master.hip")):
+    """integer values of the object-like #defines `names` of the kernel
+    sources, evaluated through the other #defines they use (so the numbers
+    bench.py reports follow the kernels' own constants)"""
+    import re
+    defs = {}
+    for fn in files:
+        with open(os.path.join(os.path.dirname(_build.SRC), fn)) as f:
+            for line in f:
+                m = re.match(r"\s*#define\s+(\w+)\s+([^/\n]+)", line)
+                if m and re.fullmatch(r"[\w\s()+\-*/%]+", m.group(2).strip()):
+                    defs.setdefault(m.group(1), m.group(2).strip())
+
+    def ev(name, depth=0):
+        expr = re.sub(r"[A-Za-z_]\w*", lambda t: "(%d)" % ev(t.group(0), depth + 1), defs[name])
+        return int(eval(expr.replace("/", "//"), {"__builtins__": {}}))
+    return {n: ev(n) for n in names}
+
+
 # kernels launched with dynamic LDS (bytes per workgroup, waves per workgroup):
 # the compiler's resource report shows 0 for them.  k_master_tail: PAC_TAIL_LDS
-# (csrc/pac_master.hip) = 22 500 B: smr, group maxima, bits, group indices, nLines,
-# the line quarters' Huffman sums;
-# four waves per workgroup
-# (pac_abi.hip run_master launch)
-DYNAMIC_LDS = {"k_master_tail": (25 * 64 * 8 + 5 * 64 * 8 + 25 * 64 + 5 * 64 + 25 * 4 + 4 * 5 * 64 * 4, 4)}
+# (csrc/pac_master.hip, 22 500 B: smr, group maxima, bits, group indices,
+# nLines, the line quarters' Huffman sums) and PAC_TAIL_Q waves per workgroup
+# (pac_abi.hip run_master launch), read from the source
+def dynamic_lds():
+    d = csrc_defines(["PAC_TAIL_LDS", "PAC_TAIL_Q"])
+    return {"k_master_tail": (d["PAC_TAIL_LDS"], d["PAC_TAIL_Q"])}
 
 # kernels whose occupancy the line reports beside the dominant one
 OCC_KERNELS = ["k_master_lrms_spec", "k_master_front", "k_master_tail", "k_origin_front", "k_master_thr_short"]
@@ -429,8 +449,9 @@ def occupancy(kind, kernels):
              "limit_waves_per_simd": r.get("occupancy_waves_per_simd"), "vgprs": r.get("vgprs"),
              "lds_bytes_per_workgroup": r.get("lds_bytes")}
         lds = r.get("lds_bytes") or 0
-        if k in DYNAMIC_LDS:          # launched with dynamic LDS: the compiler reports 0
-            lds, wg_waves = DYNAMIC_LDS[k]
+        dyn = dynamic_lds()
+        if k in dyn:                  # launched with dynamic LDS: the compiler reports 0
+            lds, wg_waves = dyn[k]
             e["lds_bytes_per_workgroup"] = lds
             e["lds_dynamic"] = True
             lim = (160 * 1024) // lds * wg_waves / 4.0       # workgroups per CU x waves each / 4 SIMDs

@@ -1038,8 +1038,14 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         const PacMasterChunkBuf K = bufset(i);
         // front_fast: the side kernel writes line set i % 3, whose last reader
         // was the tail of chunk i - 3 (recorded before this launch in every
-        // schedule; it ran beside an earlier threshold launch)
-        if (front_fast && i >= 3 && tail_done[i - 3]) HIPCHK(hipStreamWaitEvent(s2, tail_done[i - 3], 0));
+        // schedule; it ran beside an earlier threshold launch).  A schedule
+        // that launches the side kernel first would race on K.lines: refused.
+        if (front_fast && i >= 3) {
+            if (!tail_done[i - 3])
+                return set_err(PAC_E_HIP, "internal: side kernel of chunk %lld before the tail of chunk %lld",
+                               (long long)i, (long long)(i - 3));
+            HIPCHK(hipStreamWaitEvent(s2, tail_done[i - 3], 0));
+        }
         if ((rc2 = mark(2, -1))) return rc2;
         if (c->side_fused) {          // timed as the spectra phase (spec_ms), lrms_ms = 0
             if (front_fast)

@@ -265,9 +265,11 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
             // `out` in the block's six rows
             const double* bt = out - (v - 2) * PAC_HALFN;
             const double bm = bt[r * WAVE + lane], bsv = bt[PAC_HALFN + r * WAVE + lane];
-            t = v == 4 ? wave_masking_row<true>(L, nm, T, lane, r, bm, bsv)
-                       : wave_masking_row<true>(L, nm, T, lane, r, bsv, bm);
-            if (t < 0.0) {                                      // uniform
+            int gone = 0;
+            t = v == 4 ? wave_masking_row<true>(L, nm, T, lane, r, bm, bsv, &gone)
+                       : wave_masking_row<true>(L, nm, T, lane, r, bsv, bm, &gone);
+            gone = __builtin_amdgcn_readfirstlane(gone);
+            if (gone) {                                         // scalar (SCC) branch
                 if (lane == 0) atomicAnd(kept, ~(1 << (r + (v == 5 ? 16 : 0))));
                 continue;
             }
@@ -421,19 +423,27 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     }
     thr_variant(T, p, K.thr + (j * 6 + vb + 1) * PAC_HALFN, vb + 1, rows2, buf, tmp, t2, pm, 5);
     TPROF(8);
-    const unsigned long long pbase = *reinterpret_cast<volatile unsigned long long*>(park);
+    // wave-uniform by construction; readfirstlane makes it scalar for the
+    // compiler too, so that the pass below (ballots) runs under no exec mask
+    const unsigned long long pv = *reinterpret_cast<volatile unsigned long long*>(park);
+    const unsigned long long pbase = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(pv >> 32)) << 32) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane((int)pv);
     if (pbase) {
         // the MLD rows this block needs: THR_S (psychoac.py:582-591) needs
         // MLD_M where BTHR_M > BTHR_S, THR_M needs MLD_S where BTHR_S > BTHR_M
         // -- from the rows this workgroup just stored (its other waves' stores,
-        // complete after the fence + barrier, read past the L1 from the L2:
-        // no HBM re-read of the rows a launch later); each wave a quarter of
-        // the rows
-        // workgroup scope: the stores complete to this XCD's L2 (an agent-scope
-        // fence would write the whole L2 back: measured 2x slower overall)
+        // read past the L1 from the L2: no HBM re-read of the rows a launch
+        // later); each wave a quarter of the rows.  Every wave waits for its
+        // own row stores to be acknowledged by the L2 (s_waitcnt vmcnt(0):
+        // gfx9 counts stores in vmcnt; a workgroup-scope release emits no such
+        // wait in non-tgsplit mode, and an agent-scope one would also write
+        // the whole L2 back, measured 2x slower overall) before the barrier;
+        // the readers' loads are agent-scope, i.e. from the L2, after it.
+        __builtin_amdgcn_s_waitcnt(0x0f70);                 // vmcnt(0); expcnt, lgkmcnt unchanged
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         lds_sync();
-        const int lane = t2 & (WAVE - 1), w = t2 / WAVE;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int lane = t2 & (WAVE - 1), w = __builtin_amdgcn_readfirstlane(t2 / WAVE);
         const int prow = __builtin_amdgcn_readfirstlane(park[2]);
         double* blk = reinterpret_cast<double*>(pbase);
         const unsigned long long* tm = reinterpret_cast<const unsigned long long*>(blk + 2 * PAC_HALFN);
@@ -998,9 +1008,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     __shared__ double2 bufA[1024], bufB[1024];    // 32 KB
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, blockIdx.x, &cp)) return;
-    // K.mdct: set by the host only for sine-window stereo calls with block
-    // switching; the plain long frames' lines (the other frames transform in
-    // the front)
+    // K.mdct (the <false> instantiation): set by the host for sine-window
+    // stereo calls whose front is k_master_front<false> -- block switching, or
+    // PAC_SIDE_CODED=0 -- the plain long frames' lines (the other frames
+    // transform in the front).  waves_per_eu(5) holds both instantiations at
+    // 95 VGPRs with no spills (libpacgpu.resources.json, tests/test_host.py).
     // (CODED calls are stereo; the nch test is kept in both instantiations: without
     // it the compiler schedules the CODED kernel into 111 VGPRs, or 17 spills at 96)
     if (CODED && ck.nch == 2) {

@@ -1127,10 +1127,15 @@ __device__ __forceinline__ double mom_group(const MaskerLists& L, const PacTable
 // ref_hi whatever the rest of the sum, and the row returns -1 (not needed:
 // the front's +inf gives the same combination).  On the bench signal 12 of
 // the ~14 MLD_M rows of a block end here, before the loud-masker sums.
+// The decision is returned in *gone as a scalar (readfirstlane of the ballot),
+// so that the caller's skip is an SCC branch: a per-lane test of the returned
+// value would put the caller's skip / continue under an exec mask around the
+// next row's full-wave ballots and DPP (the shape of the round-5 hang).
 #define PAC_PRUNE_MARGIN 1.0000000000009095      // 1 + 2^-40
 template <bool PRUNE = false>
 __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm, const PacTables* __restrict__ T,
-                                                   int lane, int r, double ref_hi = 0.0, double ref_lo = 0.0) {
+                                                   int lane, int r, double ref_hi = 0.0, double ref_lo = 0.0,
+                                                   int* gone = nullptr) {
     const int l = r * WAVE + lane;
     const double zl = T->bark_line[l];
     const double zr = T->bark_line[r * WAVE];           // smallest z of the row
@@ -1150,7 +1155,9 @@ __device__ __forceinline__ double wave_masking_row(const MaskerLists& L, int nm,
     if constexpr (PRUNE) {
         const double lb = ((upq + flat) + lower) + tiq;
         const bool need = ref_hi > ref_lo && !(pac_mld_intensity(lb, T->mld[l]) > ref_hi * PAC_PRUNE_MARGIN);
-        if (!__ballot(need)) return -1.0;              // uniform: the row is not needed
+        const int none = __builtin_amdgcn_readfirstlane(__ballot(need) == 0ull ? 1 : 0);
+        *gone = none;
+        if (none) return 0.0;                          // scalar: the row is not needed
     }
     RP_T(t1);
     // loud maskers below the line: loud-list ranks [0, Ul)

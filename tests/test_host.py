@@ -3,6 +3,7 @@ symbol include/pac_gpu.h declares (no compute without a GPU), host mirrors of
 the reference's file-format logic, the Huffman table export, the synthetic
 generators and the stream shard planner (gloo, world_size 2)."""
 import ctypes as C
+import json
 import os
 import re
 import struct
@@ -483,3 +484,23 @@ def test_bench_spawned_rank_failure_is_fatal():
                         "--streams", "2", "--blocks-per-stream", "3"], capture_output=True, text=True, env=env,
                        timeout=300)
     assert r.returncode != 0 and r.stdout.strip() == ""
+
+
+def test_bench_tail_lds_follows_the_kernel_source():
+    """bench.py's occupancy limit of the dynamic-LDS tail comes from the
+    kernel's own PAC_TAIL_LDS / PAC_TAIL_Q: 22 500 B, 4 waves"""
+    b = _bench_module()
+    assert b.dynamic_lds() == {"k_master_tail": (22500, 4)}
+    assert b.csrc_defines(["PAC_NB", "WAVE"]) == {"PAC_NB": 25, "WAVE": 64}
+
+
+def test_side_kernels_do_not_spill():
+    """amdgpu_waves_per_eu(5) holds both k_master_lrms_spec instantiations
+    (the <false> one: block switching, PAC_SIDE_CODED=0) without VGPR spills
+    (ADVICE r05), per this build's resource report"""
+    from pac_amd import build
+    d = json.load(open(build.RESOURCES))
+    if d.get("src_hash") != build.source_hash():
+        pytest.skip("resource report of another build")
+    for k in ("k_master_lrms_spec<true>", "k_master_lrms_spec<false>", "k_master_thr"):
+        assert d["kernels"][k]["vgpr_spill"] == 0 and d["kernels"][k]["scratch_bytes_per_lane"] == 0, k

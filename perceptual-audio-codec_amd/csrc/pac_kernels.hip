@@ -274,9 +274,7 @@ __global__ __launch_bounds__(FRONT_NT, 4) void k_origin_front(PacSource src, con
     // Masking rows are claimed dynamically, most expensive first (the order
     // measured on broadband input: middle rows carry the most maskers on both
     // sides); a wave keeps its (row, threshold) pairs in registers, at most 4.
-    int* rowctr = L.misc;
-    if (tid == 0) *rowctr = 0;
-    __syncthreads();
+    int* rowctr = L.misc;                  // reset by grp_find_maskers before its last barrier
     double tv0 = 0.0, tv1 = 0.0, tv2 = 0.0, tv3 = 0.0;
     int rids = 0;                          // claimed rows, 4 bits each (wave-uniform)
     int nr = 0;

@@ -245,10 +245,9 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
     const MaskerLists L = masker_lists(buf, tmp);
     const int nm = grp_find_maskers<FRONT_NT>(reinterpret_cast<const double*>(buf), T, v >= 4 ? 0.0 : 15.0, tid, L);
     TPROF(mk + 1);
-    // rows claimed dynamically, most expensive first (as in k_origin_front)
+    // rows claimed dynamically, most expensive first (as in k_origin_front);
+    // the counter was reset by grp_find_maskers before its last barrier
     int* rowctr = L.misc;
-    if (tid == 0) *rowctr = 0;
-    lds_sync();
     __builtin_amdgcn_s_setprio(0);
 #pragma unroll 1
     while (true) {

@@ -930,7 +930,9 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
             if ((lb[q] >> lane) & 1ull) { L.lz[j] = rz[q]; L.lB[j] = rB[q]; L.lku[j] = rku[q]; }
         }
     }
-    if (tid == 0) { L.lpre[tot] = (int16_t)nloud; L.misc[1] = nloud; }
+    // the rows' claiming counter (misc[0]) reset here: visible after the scans'
+    // barrier, so the caller's row loop needs no barrier of its own
+    if (tid == 0) { L.lpre[tot] = (int16_t)nloud; L.misc[1] = nloud; L.misc[0] = 0; }
     grp_sync<NT>();
     grp_scan_lists<NT>(L, tid);
     return tot;

@@ -1,6 +1,6 @@
 """Build an A/B variant of libpacgpu.so: copy csrc/ to a temp dir, apply
-literal (old -> new) replacements, compile to variants/libpacgpu_<name>.so.
-Select it at run time with PAC_LIB=variants/libpacgpu_<name>.so.
+literal (old -> new) replacements, compile to ab/libpacgpu_<name>.so.
+Select it at run time with PAC_LIB=ab/libpacgpu_<name>.so.
 
     python tools/build_variant.py NAME FILE 'old' 'new' [FILE 'old' 'new' ...]
     python tools/build_variant.py NAME FILE @FILE path/to/replacement
@@ -29,7 +29,7 @@ def main(name, edits):
         if old not in s:
             raise SystemExit("edit not found in %s: %r" % (f, old[:60]))
         open(p, "w").write(s.replace(old, new))
-    out = os.path.join(ROOT, "variants", "libpacgpu_%s.so" % name)
+    out = os.path.join(ROOT, "ab", "libpacgpu_%s.so" % name)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
            "-shared", "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(ROOT, "include"),

@@ -6,5 +6,5 @@
 # end), 4 after the barrier, 5-7 the second variant, 8 end
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-PAC_LIB=variants/libpacgpu_thrprof.so PAC_DEBUG_FLAGS=128 timeout -k 10 120 python bench.py --no-cpu --config 2 --steps 1 --warmup 1 > gpurun_out/pt_thr.json 2> gpurun_out/pt_thr.err || exit 1
+PAC_LIB=ab/libpacgpu_thrprof.so PAC_DEBUG_FLAGS=128 timeout -k 10 120 python bench.py --no-cpu --config 2 --steps 1 --warmup 1 > gpurun_out/pt_thr.json 2> gpurun_out/pt_thr.err || exit 1
 grep -A9 PAC_PROF gpurun_out/pt_thr.err | tail -10

@@ -279,23 +279,6 @@ __device__ __forceinline__ int16_t pac_float_to_pcm(double x) {
     return s ? (int16_t)-c : c;
 }
 
-// dequantized lines of channel-block g into L (LDS), / 2^overall
-template <int NT>
-__device__ __forceinline__ void grp_dequant(const PacTables* __restrict__ T, const PacDecWork& D, int64_t g,
-                                            double* L, int tid) {
-    const int ov = D.overall[g];
-    const double rescale = 1.0 * (double)(1 << ov);
-#pragma unroll
-    for (int i = 0; i < PAC_HALFN / NT; ++i) {
-        const int l = i * NT + tid;
-        const int b = T->band_of_line[l];
-        const int ba = (l < T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1]) ? D.ba[g * PAC_NB + b] : 0;
-        double v = 0.0;
-        if (ba) v = pac_dequantize(D.sf[g * PAC_NB + b], D.codes[dec_code_at(g, l)], ba);
-        L[l] = v / rescale;
-    }
-}
-
 // IMDCT (mdct.py:72-79) of the lines in L, sine-windowed: w(n) for n < 2048
 // from U = 2 DCT-IV(L) (in buf):  n < 512: U[n+512];  512 <= n < 1536:
 // -U[1535-n];  n >= 1536: -U[n-1536]
@@ -341,14 +324,21 @@ struct PacDecOut {
     int preroll;
 };
 
-__global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__ T, PacDecWork D,
-                                                   const int64_t* __restrict__ cb_base,
-                                                   const int64_t* __restrict__ nblk,
-                                                   const int64_t* __restrict__ seg_base, int n_streams,
-                                                   int nch, int master, PacDecOut O) {
+// The synthesis holds each block's dequantized lines in registers, in the
+// order the DCT-IV's pre-twiddle reads them (lines 2q and 1023 - 2q of
+// q = tid, tid + 256: grp_dct4_regs), so the M/S reconstruction is
+// thread-local and the plain frames need no LDS copy of the lines; 40 KB of
+// LDS (FFT scratch, overlap halves, the short frames' lines) and at most 128
+// VGPRs: 4 waves per SIMD.  A stereo pair's two samples of a frame go out as
+// one 32-bit store.  Barriers hand off LDS only (lds_sync): the code loads and
+// PCM stores stay in flight across them.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dec_synth(
+    const PacTables* __restrict__ T, PacDecWork D, const int64_t* __restrict__ cb_base,
+    const int64_t* __restrict__ nblk, const int64_t* __restrict__ seg_base, int n_streams, int nch, int master,
+    PacDecOut O) {
     __shared__ double2 buf[1024];                 // IMDCT scratch
-    __shared__ double lines[2][PAC_HALFN];
-    __shared__ double prev[2][PAC_HALFN];
+    __shared__ double prev[2][PAC_HALFN];         // overlap halves (thread-private slots)
+    __shared__ double sl[PAC_HALFN];              // a short frame's lines (block switching)
     const int tid = threadIdx.x;
     const bool pair = master && nch == 2;          // M/S stereo pair (mono master: per channel)
     const int nc = pair ? 2 : 1;
@@ -361,72 +351,106 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
     const int64_t nb = nblk[s];
     const int64_t b0 = (item - seg_base[s]) * DEC_SEG;
     const int64_t b1 = b0 + DEC_SEG < nb ? b0 + DEC_SEG : nb;
-    const int64_t first_out = O.preroll ? 0 : 1;
+    // the thread's four lines (pre-twiddle order), their bands and whether a band covers them
+    const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+    auto ln = [&](int i) { const int q = (i >> 1) * 256 + tid; return (i & 1) ? 1023 - 2 * q : 2 * q; };
+    int bnd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bnd[i] = ln(i) < lend ? T->band_of_line[ln(i)] : -1;
     for (int c = 0; c < nc; ++c)
         for (int i = tid; i < PAC_HALFN; i += 256) prev[c][i] = 0.0;
-    __syncthreads();
+    const int64_t base = cb_base[s];
     for (int64_t b = b0 > 0 ? b0 - 1 : 0; b < b1; ++b) {
-        for (int c = 0; c < nc; ++c)
-            grp_dequant<256>(T, D, cb_base[s] + b * nch + c0 + c, lines[c], tid);
-        __syncthreads();
+        // vDequantize of the four lines of each channel, / 2^overall (codec.py:25-45)
+        double x[2][4];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= nc) break;
+            const int64_t g = base + b * nch + c0 + c;
+            const double rescale = 1.0 * (double)(1 << D.overall[g]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ba = bnd[i] >= 0 ? D.ba[g * PAC_NB + bnd[i]] : 0;
+                double v = 0.0;
+                if (ba) v = pac_dequantize(D.sf[g * PAC_NB + bnd[i]], D.codes[dec_code_at(g, ln(i))], ba);
+                x[c][i] = v / rescale;
+            }
+        }
         if (pair) {
             // codec.py:46-54: mdctLineL/R alias mdctLine[0]/[1]; the second
             // assignment reads the updated channel 0: L = M - S, R = (M - S) + S
-            const uint8_t* lr = D.lrms + (cb_base[s] + b * nch + 1) * PAC_NB;   // last channel's bits
+            const uint8_t* lr = D.lrms + (base + b * nch + 1) * PAC_NB;   // last channel's bits
 #pragma unroll
-            for (int i = 0; i < PAC_HALFN / 256; ++i) {
-                const int l = i * 256 + tid;
-                if (l < T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1] && lr[T->band_of_line[l]]) {
-                    const double a = lines[0][l] - lines[1][l];
-                    lines[0][l] = a;
-                    lines[1][l] = a + lines[1][l];
+            for (int i = 0; i < 4; ++i) {
+                if (bnd[i] >= 0 && lr[bnd[i]]) {
+                    const double a = x[0][i] - x[1][i];
+                    x[0][i] = a;
+                    x[1][i] = a + x[1][i];
                 }
             }
-            __syncthreads();
         }
         // block switching: this frame short, or a long frame's start / stop shape
         int fl = 0;
         if (D.bsf) {
-            const int64_t g0 = cb_base[s] + b * nch;
+            const int64_t g0 = base + b * nch;
             fl = (D.bsf[g0] ? PAC_BS_SHORT : 0) | (b > 0 && D.bsf[g0 - nch] ? PAC_BS_PREV : 0) |
                  (b + 1 < nb && D.bsf[g0 + nch] ? PAC_BS_NEXT : 0);
         }
-        for (int c = 0; c < nc; ++c) {
+        const bool out = b >= b0 && b >= 1 - (O.preroll ? 1 : 0);
+        const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
+        uint32_t h0[4] = {0u, 0u, 0u, 0u};         // a pair's channel-0 samples until channel 1's
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= nc) break;
+            lds_sync();                            // buf / sl free: the previous transform's reads are done
             const double* U;
-            if (fl & PAC_BS_SHORT) {      // wave k: U_k = 2 DCT-IV of block k, back into its line slots
-                dec_short_imdct(lines[c], T, buf, tid);
-                __syncthreads();
-                U = lines[c];
+            if (fl & PAC_BS_SHORT) {               // wave k: U_k = 2 DCT-IV of block k, back into its line slots
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sl[ln(i)] = x[c][i];
+                lds_sync();
+                dec_short_imdct(sl, T, buf, tid);
+                lds_sync();
+                U = sl;
             } else {
                 // plain FFT layout: the swizzle's index math would cost this kernel a wave per SIMD
-                U = grp_dct4<256, false>([&](int j) { return lines[c][j]; }, T, buf, tid, 2.0);
+                U = grp_dct4_regs<256, false>(x[c], T, buf, tid, 2.0);
             }
-            const int64_t ob = b - 1 + (O.preroll ? 1 : 0);
-            auto emit = [&](int i, double w0, double w1) {
-                if (b >= b0 && b >= 1 - (O.preroll ? 1 : 0)) {
-                    const double v = prev[c][i] + w0;
-                    const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
-                    O.pcm[o] = pac_float_to_pcm(v);
-                    if (O.fpcm) O.fpcm[o] = v;
-                }
+            auto emit16 = [&](int i, double w0, double w1) {      // one sample, 16-bit store
+                const double v = prev[c][i] + w0;
                 prev[c][i] = w1;
+                if (!out) return;
+                const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
+                O.pcm[o] = pac_float_to_pcm(v);
+                if (O.fpcm) O.fpcm[o] = v;
             };
             if (fl & PAC_BS_SHORT) {
 #pragma unroll 1
                 for (int i = tid; i < PAC_HALFN; i += 256)
-                    emit(i, short_synth_at(U, T, i), short_synth_at(U, T, i + PAC_HALFN));
-            } else if (fl) {               // start / stop window
+                    emit16(i, short_synth_at(U, T, i), short_synth_at(U, T, i + PAC_HALFN));
+            } else if (fl) {                       // start / stop window
 #pragma unroll 1
                 for (int i = tid; i < PAC_HALFN; i += 256)
-                    emit(i, imdct_window_at(U, T, i, fl), imdct_window_at(U, T, i + PAC_HALFN, fl));
-            } else {
+                    emit16(i, imdct_window_at(U, T, i, fl), imdct_window_at(U, T, i + PAC_HALFN, fl));
+            } else if (!pair) {
 #pragma unroll
-                for (int i0 = 0; i0 < PAC_HALFN; i0 += 256) {
-                    const int i = i0 + tid;
-                    emit(i, imdct_window_at(U, T, i, 0), imdct_window_at(U, T, i + PAC_HALFN, 0));
+                for (int k = 0; k < 4; ++k) {
+                    const int i = k * 256 + tid;
+                    emit16(i, imdct_window_at(U, T, i, 0), imdct_window_at(U, T, i + PAC_HALFN, 0));
+                }
+            } else {                               // a pair's plain frame: (L, R) as one 32-bit store
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int i = k * 256 + tid;
+                    const double v = prev[c][i] + imdct_window_at(U, T, i, 0);
+                    prev[c][i] = imdct_window_at(U, T, i + PAC_HALFN, 0);
+                    if (!out) continue;
+                    const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * 2;
+                    const uint32_t h = (uint16_t)pac_float_to_pcm(v);
+                    if (O.fpcm) O.fpcm[o + c] = v;
+                    if (c == 0) h0[k] = h;
+                    else *reinterpret_cast<uint32_t*>(O.pcm + o) = h0[k] | (h << 16);
                 }
             }
-            __syncthreads();      // U (buf) is rewritten by the next channel / block
         }
     }
     if (b1 == nb && nb > 0) {        // end of file: the saved half alone
@@ -438,5 +462,4 @@ __global__ __launch_bounds__(256) void k_dec_synth(const PacTables* __restrict__
                 if (O.fpcm) O.fpcm[o] = prev[c][i];
             }
     }
-    (void)first_out;
 }

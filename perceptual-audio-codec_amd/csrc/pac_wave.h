@@ -466,6 +466,30 @@ __device__ __forceinline__ double* grp_dct4(const V& v, const PacTables* __restr
     return X;
 }
 
+// grp_dct4 with its input already in registers, in the pre-twiddle's order:
+// x[2 i] = v(2 q), x[2 i + 1] = v(1023 - 2 q) for q = i NT + tid (no LDS
+// staging of the input).  Bit-identical to grp_dct4.
+template <int NT, bool SWZ = true>
+__device__ __forceinline__ double* grp_dct4_regs(const double (&x)[1024 / NT], const PacTables* __restrict__ T,
+                                                 double2* buf, int tid, double sc) {
+#pragma unroll
+    for (int i = 0; i < 512 / NT; ++i) {
+        const int q = i * NT + tid;
+        buf[q] = cmul(make_double2(x[2 * i], x[2 * i + 1]), T->mdct_pre[q]);
+    }
+    const double2* Y = grp_fft_stockham<9, NT, SWZ>(buf, buf + 512, T->fft_tw, tid);
+    double* X = reinterpret_cast<double*>(buf);
+#pragma unroll
+    for (int q0 = 0; q0 < 512; q0 += NT) {
+        const int q = q0 + tid;
+        const double2 y = cmul(Y[q], T->mdct_post[q]);
+        X[2 * q] = y.x * sc;
+        X[1023 - 2 * q] = -y.y * sc;
+    }
+    grp_sync<NT>();
+    return X;
+}
+
 // MDCT (mdct.py:49-82, N = 2048, 2/N in the forward transform) of the
 // sine-windowed block xs(i) = x(i) * sine[i] (window.py:27-39, applied in
 // place in codec.py:240): the DCT-IV of the folded block [a b c d] ->

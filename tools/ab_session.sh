@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 T=${MEAS_TAG:-ab}
 if [ -z "$NO_TESTS" ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q ${PYTEST_EXTRA} --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1; rc=$?; tail -2 gpurun_out/${T}_tests.log; [ $rc = 0 ] || exit $rc
+timeout -k 10 900 python -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -x -q ${PYTEST_EXTRA} --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1; rc=$?; tail -2 gpurun_out/${T}_tests.log; [ $rc = 0 ] || exit $rc
 fi
 for r in 1 2; do
   for v in "$@" cur; do

@@ -75,21 +75,29 @@ __global__ void k_dec_index(const uint8_t* __restrict__ data, const int64_t* __r
 // zero bits, so a truncated or corrupt nBytes can never make it read outside
 // the data; the caller compares the bits consumed with 8 nBytes afterwards
 // (the reference's PackedBits raises on such input).
+//
+// The words are loaded one refill AHEAD (pre): a refill takes the word loaded
+// at the previous refill and issues the load of the next, so its latency
+// overlaps the next 32 bits of decoding instead of stalling the parse.
 struct DecBits {
-    const uint32_t* w;     // aligned word stream
+    const uint32_t* w;     // aligned word stream: the next word to load (pre holds the one before it)
     const uint32_t* wend;  // first word past the channel-block
     uint64_t buf;          // next bits, MSB first
     int nbuf;
+    uint32_t pre;          // the next word, loaded ahead
     __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
     __device__ __forceinline__ uint32_t next_word() {
-        const uint32_t v = w < wend ? be(*w) : 0u;
+        const uint32_t v = pre;
+        pre = w < wend ? *w : 0u;
         ++w;
-        return v;
+        return be(v);
     }
     __device__ __forceinline__ void init(const uint8_t* p, int64_t bit0, const uint8_t* end) {
         wend = reinterpret_cast<const uint32_t*>(((uintptr_t)end + 3) & ~(uintptr_t)3);
         const uintptr_t a = (uintptr_t)p + (uintptr_t)(bit0 >> 3);
         w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        pre = w < wend ? *w : 0u;
+        ++w;
         const int skip = (int)((a & 3) * 8 + (bit0 & 7));
         buf = (uint64_t)next_word() << 32;
         nbuf = 32;
@@ -125,7 +133,7 @@ struct DecBits {
 // bits consumed so far by reader r started at payload p, bit 0
 __device__ __forceinline__ int64_t bits_consumed(const DecBits& r, const uint8_t* p) {
     const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)3;
-    const int64_t loaded = ((int64_t)((uintptr_t)r.w - a0)) * 8;     // bits loaded from a0
+    const int64_t loaded = ((int64_t)((uintptr_t)(r.w - 1) - a0)) * 8;     // bits taken into buf from a0 (pre excluded)
     return loaded - r.nbuf - (int64_t)(((uintptr_t)p & 3) * 8);
 }
 

@@ -950,6 +950,10 @@ def main():
         "avg_launch_ms": kern_ms[dom] / launches,
         "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/summarize_pmc.py), "
                         "same source hash only",
+        "traffic_calibration": "profiles/r06_fetch_calibration.json (tools/probe/fetch_calib.hip): FETCH_SIZE "
+                               "counts half the bytes of this kernel's read shapes (8 B per lane: x2.00; 4 x 16 B "
+                               "per lane: x1.99), WRITE_SIZE the bytes of its 8 B-per-lane stores exactly -- so "
+                               "traffic is a measurement (Infinity Cache hits included), not a bound",
         "traffic_per_block": traffic_pb,
         "traffic_over_alg": traffic_pb / alg_per_block if traffic_pb is not None else None,
         "traffic_source": prof_note,

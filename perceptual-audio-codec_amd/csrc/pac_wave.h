@@ -921,6 +921,10 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
         rz[q] = rB[q] = rku[q] = rE[q] = rPL[q] = rPU[q] = 0.0;
         if (idx < tot) {
             const int k = kidx[idx];
+            // the masker's table entries first, unconditionally: their global
+            // latency then overlaps the SPL's log10 (a pow_pu load under the
+            // loud test was issued after it and waited on at once)
+            const double tz = T->bark_bin[k], tpl = T->pow_pl[k], tpu = T->pow_pu[k];
             const double s = slice6_sum(pw, k, 1024);
             const double csp = 8.0 / 3.0 * 4.0 / (2048.0 * 2048.0);
             const double sp = pac_spl(csp * s);
@@ -928,11 +932,11 @@ __device__ __forceinline__ int grp_find_maskers(const double* pw, const PacTable
             lev = 0.367 * (0.0 > lev ? 0.0 : lev);       // builtin max(SPL-40, 0)
             loud = lev != 0.0;                            // else ku == KL exactly
             rB[q] = (sp - drop - 96.0) * PAC_LOG2_10_OVER_10;
-            rz[q] = T->bark_bin[k];
+            rz[q] = tz;
             rku[q] = (lev - 27.0) * PAC_LOG2_10_OVER_10;
             rE[q] = pac_exp2(rB[q]);
-            rPL[q] = rE[q] * T->pow_pl[k];                 // 2^(B + KL (z - 1/2))
-            if (!loud) rPU[q] = rE[q] * T->pow_pu[k];      // 2^(B - KL (z + 1/2))
+            rPL[q] = rE[q] * tpl;                          // 2^(B + KL (z - 1/2))
+            if (!loud) rPU[q] = rE[q] * tpu;               // 2^(B - KL (z + 1/2))
         }
         lb[q] = __ballot(loud);
         if (lane == 0) cnt2[q * NW + w] = __popcll(lb[q]);

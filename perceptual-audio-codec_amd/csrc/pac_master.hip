@@ -753,12 +753,15 @@ __global__ __launch_bounds__(256) void k_debug_mdct_dft(const PacTables* __restr
 template <bool CODED>
 __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables* __restrict__ T,
                                            const PacMasterFields& F, const ChunkPos& cp, double2* bufA,
-                                           double2* bufB, double* __restrict__ mdct) {
+                                           double2* bufB, double* __restrict__ mdct,
+                                           const BlockRef* pre = nullptr) {
     const int tid = threadIdx.x;
     const int64_t gb = cp.gb;
-    const BlockRef bL = locate_sb(src, cp.s, cp.t, gb, 0);
+    // the block's PCM references: from the caller when it has them (the fused
+    // kernel locates the block once for both of its stages)
+    const BlockRef bL = pre ? pre[0] : locate_sb(src, cp.s, cp.t, gb, 0);
     const BlockPcm rL(bL);
-    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, 1));
+    const BlockPcm rR(pre ? pre[1] : locate_sb(src, cp.s, cp.t, gb, 1));
     // the leaf and band tables, loaded before the FFTs (their round trips
     // overlap the transform instead of following it)
     const int lf = tid >> 2, sub = tid & 3;
@@ -907,6 +910,12 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
         }
     }
     if constexpr (CODED) {
+        // the lines' bands loaded before the barrier (unconditionally: under
+        // the k < lend test the load was issued after it and waited on at once)
+        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
+        int bl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bl[i] = T->band_of_line[1023 - 256 * i - tid];
         lds_sync();
         const int oL = pac_scale_factor(fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3])), 5);
         const int oR = pac_scale_factor(fmax(fmax(wmax[4], wmax[5]), fmax(wmax[6], wmax[7])), 5);
@@ -916,11 +925,10 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
             F.overall[gb * 2] = (uint8_t)oL;
             F.overall[gb * 2 + 1] = (uint8_t)oR;
         }
-        const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = 1023 - 256 * i - tid;
-            const bool ms = k < lend && ((msm >> T->band_of_line[k]) & 1u);
+            const bool ms = k < lend && ((msm >> bl[i]) & 1u);
             const double xl = __dmul_rn(cl[i], gL), xr = __dmul_rn(cr[i], gR);
             const double M = __dadd_rn(xl, xr) / 2.0, S = __dsub_rn(xl, xr) / 2.0;
             __builtin_nontemporal_store(ms ? M : xl, mdct + k);
@@ -947,14 +955,14 @@ __global__ __launch_bounds__(256) void k_master_lrms(PacSource src, const PacTab
 __device__ __forceinline__ void spec_block(const PacSource& src, const PacTables* __restrict__ T,
                                            const PacMasterChunkBuf& K, const PacMasterFields& F,
                                            const PacMasterChunk& ck, const ChunkPos& cp, int64_t j, double2* bufA,
-                                           double2* bufB) {
+                                           double2* bufB, const BlockRef* pre = nullptr) {
     const int tid = threadIdx.x;
     const int64_t gb = cp.gb;
     const int fl = F.bsf ? F.bsf[gb] : 0;
     if (fl & PAC_BS_SHORT) return;                 // k_master_thr_short's
-    const BlockRef bL = locate_sb(src, cp.s, cp.t, gb, 0);
+    const BlockRef bL = pre ? pre[0] : locate_sb(src, cp.s, cp.t, gb, 0);
     const BlockPcm rL(bL);
-    const BlockPcm rR(locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // mono: B = A, unused
+    const BlockPcm rR(pre ? pre[1] : locate_sb(src, cp.s, cp.t, gb, ck.nch == 2 ? 1 : 0));   // mono: B = A, unused
     // bins -2..1026 at o[bin + 2], written by the real split straight from its
     // registers (no LDS round trip): the mirrored edge bins X[-k] = X[2048-k] =
     // conj X[k] stored too, so the taps of k_master_thr need no index arithmetic
@@ -1014,14 +1022,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // 95 VGPRs with no spills (libpacgpu.resources.json, tests/test_host.py).
     // (CODED calls are stereo; the nch test is kept in both instantiations: without
     // it the compiler schedules the CODED kernel into 111 VGPRs, or 17 spills at 96)
+    // the block's PCM located once for both stages: after the LRMS stage's
+    // stores the spectra stage would reload the stream offsets from global
+    // memory (not provably unchanged) and wait on them
+    const BlockRef pre[2] = {locate_sb(src, cp.s, cp.t, cp.gb, 0),
+                             locate_sb(src, cp.s, cp.t, cp.gb, ck.nch == 2 ? 1 : 0)};
     if (CODED && ck.nch == 2) {
-        lrms_block<true>(src, T, F, cp, bufA, bufB, K.lines + blockIdx.x * 2 * PAC_HALFN);
+        lrms_block<true>(src, T, F, cp, bufA, bufB, K.lines + blockIdx.x * 2 * PAC_HALFN, pre);
     } else if (!CODED && ck.nch == 2) {
         const bool md = K.mdct && !(F.bsf && F.bsf[cp.gb]);
-        lrms_block<false>(src, T, F, cp, bufA, bufB, md ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr);
+        lrms_block<false>(src, T, F, cp, bufA, bufB, md ? K.mdct + blockIdx.x * 2 * PAC_HALFN : nullptr, pre);
     }
     lds_sync();                                   // the leaf sums are read before the spectra overwrite them
-    spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB);
+    spec_block(src, T, K, F, ck, cp, blockIdx.x, bufA, bufB, pre);
 }
 
 // lane i <- lane i + OFF of its DPP row (row_shl:OFF; bound_ctrl: 0 past the

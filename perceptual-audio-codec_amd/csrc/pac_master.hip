@@ -180,10 +180,21 @@ __device__ __forceinline__ void grp_variant_pow_regs(const double2* __restrict__
         double2 m[8];                                // bins k0 - 2 .. k0 + 5
         // the thread's own four bins from memory, the two on each side from the
         // neighbouring lanes (DPP wave shifts; the same values): half the loads;
-        // a wave's edge lanes load theirs
+        // a wave's edge lanes load theirs -- right after the own bins' loads,
+        // in one branch, so that one round trip covers both (loaded and
+        // combined in two branches after the shifts, they cost the variant
+        // four serial round trips)
         const int lane = tid & (WAVE - 1);
 #pragma unroll
         for (int i = 2; i < 6; ++i) m[i] = ms(i);
+        double2 ea = make_double2(0.0, 0.0), eb = ea, fa = ea, fb = ea;   // A, B of the two edge bins
+        if (lane == 0 || lane == WAVE - 1) {
+            const int o = k0 + (lane ? 6 : 0);
+            ea = S[o];
+            eb = S[o + 1];
+            fa = S[PAC_SPEC_LD + o];
+            fb = S[PAC_SPEC_LD + o + 1];
+        }
         auto sh = [](double2 x, auto ctrl) {
             constexpr int C = decltype(ctrl)::value;
             return make_double2(dpp_f64<C>(x.x, x.x), dpp_f64<C>(x.y, x.y));
@@ -192,8 +203,10 @@ __device__ __forceinline__ void grp_variant_pow_regs(const double2* __restrict__
         m[1] = sh(m[5], std::integral_constant<int, PAC_DPP_WSHR1>{});
         m[6] = sh(m[2], std::integral_constant<int, PAC_DPP_WSHL1>{});
         m[7] = sh(m[3], std::integral_constant<int, PAC_DPP_WSHL1>{});
-        if (lane == 0) { m[0] = ms(0); m[1] = ms(1); }
-        if (lane == WAVE - 1) { m[6] = ms(6); m[7] = ms(7); }
+        const double2 e0 = make_double2(0.5 * (ea.x + sg * fa.x), 0.5 * (ea.y + sg * fa.y));   // as ms()
+        const double2 e1 = make_double2(0.5 * (eb.x + sg * fb.x), 0.5 * (eb.y + sg * fb.y));
+        if (lane == 0) { m[0] = e0; m[1] = e1; }
+        if (lane == WAVE - 1) { m[6] = e0; m[7] = e1; }
         double2 h[6];                                // M h at bins k0 - 1 .. k0 + 4
 #pragma unroll
         for (int i = 0; i < 6; ++i) h[i] = hann_tap(m[i], m[i + 1], m[i + 2]);
@@ -446,15 +459,25 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         const int prow = __builtin_amdgcn_readfirstlane(park[2]);
         double* blk = reinterpret_cast<double*>(pbase);
         const unsigned long long* tm = reinterpret_cast<const unsigned long long*>(blk + 2 * PAC_HALFN);
+        // the wave's four rows loaded together (one round trip; a row this
+        // workgroup did not store is read too -- in bounds, stale -- and ignored)
+        constexpr int NQ = 16 / (FRONT_NT / WAVE);
+        double m[NQ], sv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int r = w + q * (FRONT_NT / WAVE);
+            m[q] = __builtin_bit_cast(double, __hip_atomic_load(tm + r * WAVE + lane, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT));
+            sv[q] = __builtin_bit_cast(double, __hip_atomic_load(tm + PAC_HALFN + r * WAVE + lane, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT));
+        }
         uint32_t need = 0u;
-        for (int r = w; r < 16; r += FRONT_NT / WAVE) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int r = w + q * (FRONT_NT / WAVE);
             if (!((prow >> r) & 1)) continue;
-            const double m = __builtin_bit_cast(double, __hip_atomic_load(tm + r * WAVE + lane, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT));
-            const double sv = __builtin_bit_cast(double, __hip_atomic_load(tm + PAC_HALFN + r * WAVE + lane,
-                                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (__ballot(m > sv)) need |= 1u << r;
-            if (__ballot(sv > m)) need |= 1u << (16 + r);
+            if (__ballot(m[q] > sv[q])) need |= 1u << r;
+            if (__ballot(sv[q] > m[q])) need |= 1u << (16 + r);
         }
         if (lane == 0) MLD_NEED_AT(blk + 5 * PAC_HALFN)[w] = need;
     }

@@ -344,6 +344,15 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     const PacMasterChunkBuf& K = mld ? KB : KA;
     const PacMasterChunk& ck = mld ? ckB : ckA;
     const int vb = 2 * pi;
+    const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
+    // the M/S pair's first variant's |V|^2 straight away: its spectrum loads
+    // then overlap the block lookup and the row-mask load below (three serial
+    // round trips); an M/S pair nearly always has rows on stereo input (a
+    // skipped one wastes the loads; the L/R and MLD pairs, often skipped,
+    // load after their row masks)
+    double p[4];
+    const bool early = !mld && vb == 2 && ck.nch == 2;
+    if (early) grp_variant_pow_regs<FRONT_NT>(spec, 2, tid, p);
     ChunkPos cp;
     if (!chunk_block(src.blk_off, ck, j, &cp)) return;     // uniform per workgroup
     const int64_t gb = cp.gb;
@@ -362,7 +371,6 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     }
     rows = __builtin_amdgcn_readfirstlane(rows);
     if (!rows) return;
-    const double2* spec = K.spec + j * 2 * PAC_SPEC_LD;
     // phase clocks (PAC_DEBUG_FLAGS 128) only in a -DPAC_THR_PROF build: their
     // pointer would cost the kernel the SGPRs that keep it at 104 VGPRs
 #ifdef PAC_THR_PROF
@@ -393,7 +401,6 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         }
     }
     // the variant's |V[k]|^2 from the block's spectra of a and b (k_master_spec)
-    double p[4];
     int* kept = masker_lists(buf, tmp).misc + 2;            // the MLD workgroup's surviving rows (above)
     if (mld) {         // the MLD pair (mode 1): both variants pruned, the surviving rows written back
         double* o4 = K.thr + (j * 6 + 4) * PAC_HALFN;
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         return;
     }
     if (rows) {
-        grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
+        if (!early) grp_variant_pow_regs<FRONT_NT>(spec, vb, tid, p);
         thr_variant(T, p, K.thr + (j * 6 + vb) * PAC_HALFN, vb, rows, buf, tmp, tid, pm, 1);
     }
     if (ck.nch != 2 || !rows2) return;

@@ -370,6 +370,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int64_t base = cb_base[s];
     for (int64_t b = b0 > 0 ? b0 - 1 : 0; b < b1; ++b) {
         // vDequantize of the four lines of each channel, / 2^overall (codec.py:25-45)
+        // every field loaded unconditionally (a line past the last band reads
+        // band 0's and discards it): the loads of a block are one round trip,
+        // not ba's and then, under "ba != 0", the scale factor's and code's
         double x[2][4];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -378,9 +381,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             const double rescale = 1.0 * (double)(1 << D.overall[g]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int ba = bnd[i] >= 0 ? D.ba[g * PAC_NB + bnd[i]] : 0;
-                double v = 0.0;
-                if (ba) v = pac_dequantize(D.sf[g * PAC_NB + bnd[i]], D.codes[dec_code_at(g, ln(i))], ba);
+                const int bi = bnd[i] >= 0 ? bnd[i] : 0;
+                const int ba0 = D.ba[g * PAC_NB + bi];
+                const int sf = D.sf[g * PAC_NB + bi];
+                const int code = D.codes[dec_code_at(g, ln(i))];
+                const int ba = bnd[i] >= 0 ? ba0 : 0;
+                const double v = ba ? pac_dequantize(sf, code, ba) : 0.0;
                 x[c][i] = v / rescale;
             }
         }
@@ -388,9 +394,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             // codec.py:46-54: mdctLineL/R alias mdctLine[0]/[1]; the second
             // assignment reads the updated channel 0: L = M - S, R = (M - S) + S
             const uint8_t* lr = D.lrms + (base + b * nch + 1) * PAC_NB;   // last channel's bits
+            int lf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lf[i] = lr[bnd[i] >= 0 ? bnd[i] : 0];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if (bnd[i] >= 0 && lr[bnd[i]]) {
+                if (bnd[i] >= 0 && lf[i]) {
                     const double a = x[0][i] - x[1][i];
                     x[0][i] = a;
                     x[1][i] = a + x[1][i];

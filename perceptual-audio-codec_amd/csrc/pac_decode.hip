@@ -93,9 +93,13 @@ struct DecBits {
         return be(v);
     }
     __device__ __forceinline__ void init(const uint8_t* p, int64_t bit0, const uint8_t* end) {
-        wend = reinterpret_cast<const uint32_t*>(((uintptr_t)end + 3) & ~(uintptr_t)3);
-        const uintptr_t a = (uintptr_t)p + (uintptr_t)(bit0 >> 3);
-        w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        // pointer arithmetic from p and end only (no integer round trip): the
+        // compiler then keeps them global pointers and reads through
+        // global_load, not flat loads (whose waits also drain the LDS lookups)
+        wend = reinterpret_cast<const uint32_t*>(end + ((4 - ((uintptr_t)end & 3)) & 3));
+        const uint8_t* q = p + (bit0 >> 3);
+        const uintptr_t a = (uintptr_t)q;
+        w = reinterpret_cast<const uint32_t*>(q - (a & 3));
         pre = w < wend ? *w : 0u;
         ++w;
         const int skip = (int)((a & 3) * 8 + (bit0 & 7));

@@ -917,9 +917,9 @@ static int run_master(pac_ctx* c, const pac_params* p, PacTables* T, PacSource s
         F.codes = c->m_codes.p;
     } else {
         // staging: the output's capacity (at most a 1.5 KB average per
-        // channel-block -- the bit budget gives ~300 B) + 4 B of alignment
-        // padding per channel-block; a larger need is detected after the call
-        int64_t cap = std::min<int64_t>(out_cap, G * 1536) + 4 * G + 64 + c->stg_bias;
+        // channel-block -- the bit budget gives ~300 B) + the burst
+        // padding per channel-block (k_master_emit); a larger need is detected after the call
+        int64_t cap = std::min<int64_t>(out_cap, G * 1536) + 4 * PAC_EMIT_WORDS * G + 64 + c->stg_bias;
         if (c->stg_cap_max > 0) cap = std::min<int64_t>(cap, c->stg_bias + c->stg_cap_max);
         if ((rc = c->m_ccodes.ensure(2 * cbmax * 2 * PAC_HALFN)) || (rc = c->m_stg.ensure(cap)) ||
             (rc = c->m_stoff.ensure(G + 1)) || (rc = c->m_stg_next.ensure(1)))

@@ -78,8 +78,8 @@ struct PacMasterFields {
     const uint8_t* bsf;  // [nblocks] PAC_BS_* flags (block-switching extension), or null: off
     uint32_t* rowm;      // [nblocks] 64-line rows of L/R-coded bands (bits 0-15), M/S-coded (16-31), k_master_lrms
     // the tail's bitstream emission (null: k_master_pack packs from `codes`):
-    // each channel-block's '<L' nBytes + payload at stg + stoff[g] (4-byte
-    // aligned, padded to 4), placed at its file offset by k_master_place
+    // each channel-block's '<L' nBytes + payload at stg + stoff[g] (16-byte
+    // aligned, padded to 16), placed at its file offset by k_master_place
     uint8_t* stg;
     int64_t* stoff;      // [G]
     unsigned long long* stg_next;   // bump allocator of stg
@@ -1459,22 +1459,54 @@ __device__ __forceinline__ int wave_excl_scan_i(int v, int* total) {
     return x - v;
 }
 
-// MSB-first bit writer of one lane into 4-byte-aligned memory (big-endian
-// words: the bytes in file order)
-struct LaneBits {
-    uint32_t* w;
+// MSB-first bit writer of one lane (big-endian words: the bytes in file
+// order) whose words leave in bursts of PAC_EMIT_WORDS: the finished words of
+// a burst wait in registers (b[], oldest first) and go out with its last one
+// as 16-byte stores.  One lane per channel-block writes 64 different lines per
+// store instruction, and a line the L2 evicts half-written costs a partial
+// write: a 4-byte store per word wrote 4.56 KB per block (592 B of
+// bitstream), bursts of 4 words 1.89 KB, of 8 words 0.97 KB (PMC WRITE_SIZE,
+// configs[2]); emission VALU 530 -> 745 -> 863 per block, and the threshold
+// kernel beside it 799 -> 787 ms per 10^7 blocks (fewer store instructions).
+// The region starts 16-byte aligned and is padded to a whole burst
+// (k_master_emit, k_master_place).
+#ifndef PAC_EMIT_WORDS
+#define PAC_EMIT_WORDS 8  // words per lane store burst (a multiple of 4)
+#endif
+struct LaneBits16 {
+    static constexpr int NW = PAC_EMIT_WORDS;
+    static_assert(NW % 4 == 0, "bursts of whole 16-byte stores");
+    uint4* w;
     uint64_t acc;
-    int n;
+    int n, nw;
+    uint32_t b[NW - 1];
+    __device__ __forceinline__ void word(uint32_t x) {
+        if (nw == NW - 1) {
+#pragma unroll
+            for (int k = 0; k + 4 <= NW - 1; k += 4) w[k / 4] = make_uint4(b[k], b[k + 1], b[k + 2], b[k + 3]);
+            w[NW / 4 - 1] = make_uint4(b[NW - 4], b[NW - 3], b[NW - 2], x);
+            w += NW / 4;
+            nw = 0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < NW - 2; ++k) b[k] = b[k + 1];
+            b[NW - 2] = x;
+            ++nw;
+        }
+    }
     __device__ __forceinline__ void put(uint32_t v, int bits) {    // bits <= 32, v < 2^bits
         acc = (acc << bits) | v;
         n += bits;
         if (n >= 32) {
             n -= 32;
-            *w++ = __builtin_bswap32((uint32_t)(acc >> n));
+            word(__builtin_bswap32((uint32_t)(acc >> n)));
         }
     }
     __device__ __forceinline__ void flush() {
-        if (n > 0) *w = __builtin_bswap32((uint32_t)(acc << (32 - n)));
+        if (n > 0) word(__builtin_bswap32((uint32_t)(acc << (32 - n))));
+        // the last nw words (b[NW-1-nw] ..), then padding: zeros shifted in
+        // until the burst completes
+        while (nw > 0) word(0u);
     }
 };
 
@@ -1868,7 +1900,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int64_t gb = act ? cp.gb : 0;
     const int64_t g = gb * nch + ch, gl = j * 2 + ch;
     const int nb = act ? F.nbytes[g] : 0;
-    const int sz = act ? 4 + ((nb - 4 + 3) & ~3) : 0;
+    const int sz = act ? (nb + 4 * PAC_EMIT_WORDS - 1) & -(4 * PAC_EMIT_WORDS) : 0;   // LaneBits16 bursts
     int tot;
     const int pre = wave_excl_scan_i(sz, &tot);
     unsigned long long base = 0;
@@ -1885,9 +1917,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int tb = F.tid[g] - 1;
     uint32_t lrms_rev = 0;                                   // band 0 first
     for (int b = 0; b < PAC_NB; ++b) lrms_rev = (lrms_rev << 1) | (uint32_t)(F.lrms[gb * PAC_NB + b] & 1);
-    uint32_t* w = reinterpret_cast<uint32_t*>(F.stg + so);
-    w[0] = (uint32_t)(nb - 4);
-    LaneBits out{w + 1, 0ull, 0};
+    LaneBits16 out{reinterpret_cast<uint4*>(F.stg + so), 0ull, 0, 0, {}};
+    out.word((uint32_t)(nb - 4));                            // '<L' nBytes
     out.put(((uint32_t)F.overall[g] << 4) | (uint32_t)(tb + 1), 8);
     const uint32_t eb = H->esc_bits[tb];
     const int el = H->esc_len[tb];
@@ -1951,7 +1982,7 @@ __global__ __launch_bounds__(256) void k_master_place(PacMasterFields F, int64_t
     const int nb = F.nbytes[g];
     const int64_t og = off[g], so = F.stoff[g];
     // k_master_emit's padded size: a channel-block it skipped is skipped here too
-    if (og + nb > cap || so + (4 + ((nb - 4 + 3) & ~3)) > F.stg_cap) return;
+    if (og + nb > cap || so + ((nb + 4 * PAC_EMIT_WORDS - 1) & -(4 * PAC_EMIT_WORDS)) > F.stg_cap) return;
     const uint8_t* src = F.stg + so;
     uint8_t* dst = out + og;
     for (int i = lane; i < nb; i += WAVE) dst[i] = src[i];

@@ -76,19 +76,20 @@ __global__ void k_dec_index(const uint8_t* __restrict__ data, const int64_t* __r
 // the data; the caller compares the bits consumed with 8 nBytes afterwards
 // (the reference's PackedBits raises on such input).
 //
-// The words are loaded one refill AHEAD (pre): a refill takes the word loaded
-// at the previous refill and issues the load of the next, so its latency
-// overlaps the next 32 bits of decoding instead of stalling the parse.
+// The words are loaded two refills AHEAD (pre, pre2): a refill takes the word
+// loaded two refills before and issues the load of the next, so its latency
+// overlaps the next 64 bits of decoding instead of stalling the parse.
 struct DecBits {
-    const uint32_t* w;     // aligned word stream: the next word to load (pre holds the one before it)
+    const uint32_t* w;     // aligned word stream: the next word to load (pre, pre2 hold the two before it)
     const uint32_t* wend;  // first word past the channel-block
     uint64_t buf;          // next bits, MSB first
     int nbuf;
-    uint32_t pre;          // the next word, loaded ahead
+    uint32_t pre, pre2;    // the next two words, loaded ahead
     __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
     __device__ __forceinline__ uint32_t next_word() {
         const uint32_t v = pre;
-        pre = w < wend ? *w : 0u;
+        pre = pre2;
+        pre2 = w < wend ? *w : 0u;
         ++w;
         return be(v);
     }
@@ -101,7 +102,8 @@ struct DecBits {
         const uintptr_t a = (uintptr_t)q;
         w = reinterpret_cast<const uint32_t*>(q - (a & 3));
         pre = w < wend ? *w : 0u;
-        ++w;
+        pre2 = w + 1 < wend ? w[1] : 0u;
+        w += 2;
         const int skip = (int)((a & 3) * 8 + (bit0 & 7));
         buf = (uint64_t)next_word() << 32;
         nbuf = 32;
@@ -137,7 +139,7 @@ struct DecBits {
 // bits consumed so far by reader r started at payload p, bit 0
 __device__ __forceinline__ int64_t bits_consumed(const DecBits& r, const uint8_t* p) {
     const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)3;
-    const int64_t loaded = ((int64_t)((uintptr_t)(r.w - 1) - a0)) * 8;     // bits taken into buf from a0 (pre excluded)
+    const int64_t loaded = ((int64_t)((uintptr_t)(r.w - 2) - a0)) * 8;     // bits taken into buf from a0 (pre, pre2 excluded)
     return loaded - r.nbuf - (int64_t)(((uintptr_t)p & 3) * 8);
 }
 
@@ -270,14 +272,16 @@ __global__ __launch_bounds__(DEC_PARSE_NT) void k_dec_parse(const uint8_t* __res
 }
 
 // vDequantize (quantize.py:345-376) + vDequantizeUniform (:118-145), 4 scale bits
-__device__ __forceinline__ double pac_dequantize(int scale, int64_t m, int ba) {
-    const int64_t smask = (int64_t)1 << (ba - 1);
+// (32-bit integers: a code has ba <= 16 bits, so q < 2^30 and the largest
+// code 2^(ba+15) - 1 < 2^31 -- the same integers as the reference's, one
+// conversion each)
+__device__ __forceinline__ double pac_dequantize(int scale, int m, int ba) {
+    const int smask = 1 << (ba - 1);
     const bool neg = (m & smask) == smask;
     if (neg) m -= smask;
-    int64_t q = m << (15 - scale);
-    if (scale < 15 && m > 0) q += (int64_t)1 << (14 - scale);
-    const int64_t sm = (int64_t)1 << (ba + 14);
-    const double largest = (double)(sm << 1) - 1.0;
+    int q = m << (15 - scale);
+    if (scale < 15 && m > 0) q += 1 << (14 - scale);
+    const double largest = (double)((1u << (ba + 15)) - 1u);
     const double a = (2.0 * (double)q) / largest;
     return neg ? -a : a;
 }
@@ -286,7 +290,9 @@ __device__ __forceinline__ double pac_dequantize(int scale, int64_t m, int ba) {
 __device__ __forceinline__ int16_t pac_float_to_pcm(double x) {
     const bool s = __builtin_signbit(x);
     const double a = s ? -x : x;
-    const uint64_t code = a < 1.0 ? (uint64_t)((a * 65535.0 + 1.0) / 2.0) : 32767u;
+    // a < 1: the value is below 2^15, so the 32-bit truncating conversion (one
+    // v_cvt_u32_f64) equals the reference's integer cast
+    const uint32_t code = a < 1.0 ? (uint32_t)((a * 65535.0 + 1.0) / 2.0) : 32767u;
     const int16_t c = (int16_t)code;
     return s ? (int16_t)-c : c;
 }
@@ -393,7 +399,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         for (int c = 0; c < 2; ++c) {
             if (c >= nc) break;
             const int64_t g = base + b * nch + c0 + c;
-            const double rescale = 1.0 * (double)(1 << D.overall[g]);
+            // / 2^overall as * 2^-overall: a power of two, the same double
+            // (the lines are far from the subnormal range), one multiply
+            // instead of a division sequence per line
+            const double unscale = __builtin_ldexp(1.0, -(int)D.overall[g]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int bi = bnd[i] >= 0 ? bnd[i] : 0;
@@ -402,7 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 const int code = D.codes[dec_code_at(g, ln(i))];
                 const int ba = bnd[i] >= 0 ? ba0 : 0;
                 const double v = ba ? pac_dequantize(sf, code, ba) : 0.0;
-                x[c][i] = v / rescale;
+                x[c][i] = v * unscale;
             }
         }
         if (pair) {

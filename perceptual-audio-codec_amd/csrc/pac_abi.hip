@@ -1679,8 +1679,8 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
     const int64_t G1 = G > 0 ? G : 1;
     if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(((G1 + DEC_PARSE_NT - 1) / DEC_PARSE_NT) * DEC_PARSE_NT * PAC_HALFN)) ||
-        (rc = c->dec_ba.ensure(G1 * PAC_NB)) || (rc = c->dec_sf.ensure(G1 * PAC_NB)) ||
-        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * PAC_NB)) || (rc = c->dec_err.ensure(1)) ||
+        (rc = c->dec_ba.ensure(G1 * DEC_NBP)) || (rc = c->dec_sf.ensure(G1 * DEC_NBP)) ||
+        (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * DEC_NBP)) || (rc = c->dec_err.ensure(1)) ||
         (p->block_switch && (rc = c->dec_bsf.ensure(G1))))
         return rc;
     HIPCHK(hipMemsetAsync(c->dec_err.p, 0, sizeof(int), s));

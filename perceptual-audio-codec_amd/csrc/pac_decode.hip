@@ -38,7 +38,7 @@ struct PacHuffDec {
     int32_t sbase;
 };
 
-#define DEC_SEG 64      // blocks per synthesis workgroup (+1 preroll block each: 16 -> 64 measured +2 %)
+#define DEC_SEG 128     // blocks per synthesis workgroup (+1 preroll block each: 16 -> 64 measured +2 %, 64 -> 128 +0.9 %, 256 as 128)
 
 __global__ void k_dec_count(const uint8_t* __restrict__ data, const int64_t* __restrict__ so, int n,
                             int64_t* __restrict__ cnt) {
@@ -161,8 +161,10 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
 }
 
 // Per-channel-block fields: codes (signed mantissa codes as the reference's
-// ReadDataBlock builds them, layout dec_code_at), ba/sf [G][25], overall [G],
-// lrms [G][25] (master).
+// ReadDataBlock builds them, layout dec_code_at), ba/sf [G][DEC_NBP], overall
+// [G], lrms [G][DEC_NBP] (master) -- rows of 28 bytes, so that the parse writes
+// a channel-block's 25 bands as seven 32-bit words per field instead of 25
+// byte stores.
 //
 // The codes are tiled: tile (g / 64, l / 8) holds lines l .. l+7 of the 64
 // channel-blocks g of one parse wave as 64 runs of 8 codes (1 KB).  The parse
@@ -173,6 +175,7 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
 // open lines than the L2 holds: the parse wrote 41.4 KB to HBM per block for
 // 4 KB of codes.)  The synthesis reads 16 contiguous bytes per 8 threads.
 #define DEC_GRP 8
+#define DEC_NBP 28      // bytes per channel-block row of ba / sf / lrms (25 bands, word-padded)
 __device__ __forceinline__ int64_t dec_code_at(int64_t g, int l) {
     return (((g >> 6) * (PAC_HALFN / DEC_GRP) + (l / DEC_GRP)) * (WAVE * DEC_GRP)) + ((g & 63) * DEC_GRP) +
            (l % DEC_GRP);
@@ -222,13 +225,19 @@ __global__ __launch_bounds__(DEC_PARSE_NT) void k_dec_parse(const uint8_t* __res
             *reinterpret_cast<uint4*>(D.codes + dec_code_at(g, gcur * DEC_GRP)) = *reinterpret_cast<const uint4*>(st);
     };
     int64_t bit = master ? 8 : 4;         // bit position, for the sign-bit reader
+    uint32_t baw = 0u, sfw = 0u;          // four bands' ba / sf bytes, stored as words
     for (int b = 0; b < PAC_NB; ++b) {
         int a = (int)r.read(4);
         if (a) a++;
         const uint32_t sfv = r.read(4);
-        if (valid) {
-            D.ba[g * PAC_NB + b] = (uint8_t)a;
-            D.sf[g * PAC_NB + b] = (uint8_t)sfv;
+        baw |= (uint32_t)a << (8 * (b & 3));
+        sfw |= sfv << (8 * (b & 3));
+        if ((b & 3) == 3 || b == PAC_NB - 1) {   // uniform
+            if (valid) {
+                *reinterpret_cast<uint32_t*>(D.ba + g * DEC_NBP + (b & ~3)) = baw;
+                *reinterpret_cast<uint32_t*>(D.sf + g * DEC_NBP + (b & ~3)) = sfw;
+            }
+            baw = sfw = 0u;
         }
         bit += 8;
         if (!__ballot(a != 0)) continue;   // no lane codes the band
@@ -259,9 +268,13 @@ __global__ __launch_bounds__(DEC_PARSE_NT) void k_dec_parse(const uint8_t* __res
     }
     flush();
     if (master) {
+        uint32_t fw = 0u;
         for (int b = 0; b < PAC_NB; ++b) {
-            const uint32_t f = r.read(1);
-            if (valid) D.lrms[g * PAC_NB + b] = (uint8_t)f;
+            fw |= r.read(1) << (8 * (b & 3));
+            if ((b & 3) == 3 || b == PAC_NB - 1) {
+                if (valid) *reinterpret_cast<uint32_t*>(D.lrms + g * DEC_NBP + (b & ~3)) = fw;
+                fw = 0u;
+            }
         }
     }
     if (D.bsf) {
@@ -406,8 +419,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int bi = bnd[i] >= 0 ? bnd[i] : 0;
-                const int ba0 = D.ba[g * PAC_NB + bi];
-                const int sf = D.sf[g * PAC_NB + bi];
+                const int ba0 = D.ba[g * DEC_NBP + bi];
+                const int sf = D.sf[g * DEC_NBP + bi];
                 const int code = D.codes[dec_code_at(g, ln(i))];
                 const int ba = bnd[i] >= 0 ? ba0 : 0;
                 const double v = ba ? pac_dequantize(sf, code, ba) : 0.0;
@@ -417,7 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (pair) {
             // codec.py:46-54: mdctLineL/R alias mdctLine[0]/[1]; the second
             // assignment reads the updated channel 0: L = M - S, R = (M - S) + S
-            const uint8_t* lr = D.lrms + (base + b * nch + 1) * PAC_NB;   // last channel's bits
+            const uint8_t* lr = D.lrms + (base + b * nch + 1) * DEC_NBP;   // last channel's bits
             int lf[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) lf[i] = lr[bnd[i] >= 0 ? bnd[i] : 0];

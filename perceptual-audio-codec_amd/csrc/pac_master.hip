@@ -79,7 +79,7 @@ struct PacMasterFields {
     uint32_t* rowm;      // [nblocks] 64-line rows of L/R-coded bands (bits 0-15), M/S-coded (16-31), k_master_lrms
     // the tail's bitstream emission (null: k_master_pack packs from `codes`):
     // each channel-block's '<L' nBytes + payload at stg + stoff[g] (16-byte
-    // aligned, padded to 16), placed at its file offset by k_master_place
+    // aligned, padded to a whole LaneBits16 burst), placed at its file offset by k_master_place
     uint8_t* stg;
     int64_t* stoff;      // [G]
     unsigned long long* stg_next;   // bump allocator of stg

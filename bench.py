@@ -356,7 +356,11 @@ def measured_profile(kind, kernel):
     rel = os.path.relpath(files[-1], ROOT)
     if d.get("src_hash") != _build.source_hash():
         return None, "%s is stale (src_hash %s, this build %s)" % (rel, d.get("src_hash"), _build.source_hash())
-    k = d.get("kernels", {}).get(kernel) or d.get("kernels", {}).get("void " + kernel)   # templates: "void k<..>"
+    ks = d.get("kernels", {})
+    k = ks.get(kernel) or ks.get("void " + kernel)   # templates: "void k<..>"
+    if not k:                                        # a template named without its arguments: the one instantiation profiled
+        inst = [v for n, v in ks.items() if n.startswith("void " + kernel + "<")]
+        k = inst[0] if len(inst) == 1 else None
     if not k or not k.get("derived"):
         return None, "%s has no counters for %s" % (rel, kernel)
     out = dict(k["derived"])

@@ -1719,9 +1719,14 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
         if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
         PacDecOut O{pdev, fdev, c->dec_fo.p, preroll ? 1 : 0};
         const int64_t grid = segs * (master ? 1 : nch);
-        if (grid > 0)
-            hipLaunchKernelGGL(k_dec_synth, dim3((unsigned)grid), dim3(256), 0, s, T, D, c->dec_cbbase.p,
-                               c->dec_nblk.p, c->dec_segbase.p, n_streams, nch, (int)master, O);
+        if (grid > 0) {     // the block-switching instantiation only when the stream has the flags
+            if (D.bsf)
+                hipLaunchKernelGGL(k_dec_synth<true>, dim3((unsigned)grid), dim3(256), 0, s, T, D, c->dec_cbbase.p,
+                                   c->dec_nblk.p, c->dec_segbase.p, n_streams, nch, (int)master, O);
+            else
+                hipLaunchKernelGGL(k_dec_synth<false>, dim3((unsigned)grid), dim3(256), 0, s, T, D, c->dec_cbbase.p,
+                                   c->dec_nblk.p, c->dec_segbase.p, n_streams, nch, (int)master, O);
+        }
         HIPCHK(hipGetLastError());
     } else if (c->timing) {
         HIPCHK(hipEventRecord(c->ev[1], s));

@@ -358,18 +358,21 @@ struct PacDecOut {
 // The synthesis holds each block's dequantized lines in registers, in the
 // order the DCT-IV's pre-twiddle reads them (lines 2q and 1023 - 2q of
 // q = tid, tid + 256: grp_dct4_regs), so the M/S reconstruction is
-// thread-local and the plain frames need no LDS copy of the lines; 40 KB of
-// LDS (FFT scratch, overlap halves, the short frames' lines) and at most 128
-// VGPRs: 4 waves per SIMD.  A stereo pair's two samples of a frame go out as
-// one 32-bit store.  Barriers hand off LDS only (lds_sync): the code loads and
-// PCM stores stay in flight across them.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_dec_synth(
+// thread-local and the plain frames need no LDS copy of the lines.  A stereo
+// pair's two samples of a frame go out as one 32-bit store.  Barriers hand off
+// LDS only (lds_sync): the code loads and PCM stores stay in flight across
+// them.  BS (block switching on): 40 KB of LDS (FFT scratch, overlap halves,
+// the short frames' lines) and at most 128 VGPRs, 4 waves per SIMD; without
+// it the short and start / stop frames' code is gone: 32 KB and 91 VGPRs, 5
+// waves per SIMD.
+template <bool BS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5))) void k_dec_synth(
     const PacTables* __restrict__ T, PacDecWork D, const int64_t* __restrict__ cb_base,
     const int64_t* __restrict__ nblk, const int64_t* __restrict__ seg_base, int n_streams, int nch, int master,
     PacDecOut O) {
     __shared__ double2 buf[1024];                 // IMDCT scratch
     __shared__ double prev[2][PAC_HALFN];         // overlap halves (thread-private slots)
-    __shared__ double sl[PAC_HALFN];              // a short frame's lines (block switching)
+    __shared__ double sl[BS ? PAC_HALFN : 1];     // a short frame's lines (block switching)
     const int tid = threadIdx.x;
     const bool pair = master && nch == 2;          // M/S stereo pair (mono master: per channel)
     const int nc = pair ? 2 : 1;
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
         // block switching: this frame short, or a long frame's start / stop shape
         int fl = 0;
-        if (D.bsf) {
+        if (BS && D.bsf) {
             const int64_t g0 = base + b * nch;
             fl = (D.bsf[g0] ? PAC_BS_SHORT : 0) | (b > 0 && D.bsf[g0 - nch] ? PAC_BS_PREV : 0) |
                  (b + 1 < nb && D.bsf[g0 + nch] ? PAC_BS_NEXT : 0);
@@ -458,7 +461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             if (c >= nc) break;
             lds_sync();                            // buf / sl free: the previous transform's reads are done
             const double* U;
-            if (fl & PAC_BS_SHORT) {               // wave k: U_k = 2 DCT-IV of block k, back into its line slots
+            if (BS && (fl & PAC_BS_SHORT)) {       // wave k: U_k = 2 DCT-IV of block k, back into its line slots
 #pragma unroll
                 for (int i = 0; i < 4; ++i) sl[ln(i)] = x[c][i];
                 lds_sync();
@@ -477,11 +480,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 O.pcm[o] = pac_float_to_pcm(v);
                 if (O.fpcm) O.fpcm[o] = v;
             };
-            if (fl & PAC_BS_SHORT) {
+            if (BS && (fl & PAC_BS_SHORT)) {
 #pragma unroll 1
                 for (int i = tid; i < PAC_HALFN; i += 256)
                     emit16(i, short_synth_at(U, T, i), short_synth_at(U, T, i + PAC_HALFN));
-            } else if (fl) {                       // start / stop window
+            } else if (BS && fl) {                 // start / stop window
 #pragma unroll 1
                 for (int i = tid; i < PAC_HALFN; i += 256)
                     emit16(i, imdct_window_at(U, T, i, fl), imdct_window_at(U, T, i + PAC_HALFN, fl));

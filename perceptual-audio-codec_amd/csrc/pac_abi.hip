@@ -1679,7 +1679,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     if (G > 0x7fffffffLL) return set_err(PAC_E_ARG, "too many channel-blocks in one call");
     const int64_t G1 = G > 0 ? G : 1;
     if ((rc = c->dec_cboff.ensure(G1)) || (rc = c->dec_codes.ensure(((G1 + DEC_PARSE_NT - 1) / DEC_PARSE_NT) * DEC_PARSE_NT * PAC_HALFN)) ||
-        (rc = c->dec_ba.ensure(G1 * DEC_NBP)) || (rc = c->dec_sf.ensure(G1 * DEC_NBP)) ||
+        (rc = c->dec_ba.ensure(G1 * DEC_NBP * 2)) ||
         (rc = c->dec_ov.ensure(G1)) || (rc = c->dec_lrms.ensure(G1 * DEC_NBP)) || (rc = c->dec_err.ensure(1)) ||
         (p->block_switch && (rc = c->dec_bsf.ensure(G1))))
         return rc;
@@ -1710,7 +1710,7 @@ extern "C" int pac_decode_streams(pac_ctx* c, const pac_params* p, int32_t n_str
     if (G) {
         hipLaunchKernelGGL(k_dec_index, dim3((n_streams + 255) / 256), dim3(256), 0, s, ddev, c->dec_so.p, n_streams,
                            c->dec_cbbase.p, c->dec_cboff.p);
-        PacDecWork D{c->dec_codes.p, c->dec_ba.p, c->dec_sf.p, c->dec_ov.p, c->dec_lrms.p, c->dec_err.p,
+        PacDecWork D{c->dec_codes.p, reinterpret_cast<uint16_t*>(c->dec_ba.p), c->dec_ov.p, c->dec_lrms.p, c->dec_err.p,
                      p->block_switch ? c->dec_bsf.p : nullptr};
         hipLaunchKernelGGL(k_dec_parse, dim3((unsigned)((G + DEC_PARSE_NT - 1) / DEC_PARSE_NT)), dim3(DEC_PARSE_NT), 0, s,
                            ddev, c->dec_cboff.p, G,

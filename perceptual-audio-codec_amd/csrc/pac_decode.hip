@@ -161,10 +161,10 @@ __device__ __forceinline__ uint32_t dec_huff(DecBits& r, const uint32_t* __restr
 }
 
 // Per-channel-block fields: codes (signed mantissa codes as the reference's
-// ReadDataBlock builds them, layout dec_code_at), ba/sf [G][DEC_NBP], overall
-// [G], lrms [G][DEC_NBP] (master) -- rows of 28 bytes, so that the parse writes
-// a channel-block's 25 bands as seven 32-bit words per field instead of 25
-// byte stores.
+// ReadDataBlock builds them, layout dec_code_at), basf [G][DEC_NBP] (ba | sf <<
+// 8), overall [G], lrms [G][DEC_NBP] (master) -- rows of 28 entries, so that
+// the parse writes a channel-block's 25 bands as 32-bit words (14 for basf,
+// 7 for lrms) instead of one store per band and field.
 //
 // The codes are tiled: tile (g / 64, l / 8) holds lines l .. l+7 of the 64
 // channel-blocks g of one parse wave as 64 runs of 8 codes (1 KB).  The parse
@@ -182,8 +182,7 @@ __device__ __forceinline__ int64_t dec_code_at(int64_t g, int l) {
 }
 struct PacDecWork {
     uint16_t* codes;
-    uint8_t* ba;
-    uint8_t* sf;
+    uint16_t* basf;     // [G][DEC_NBP] ba | sf << 8 (one load per line in the synthesis)
     uint8_t* overall;
     uint8_t* lrms;
     int* err;           // set to 1 when a channel-block's fields run past its nBytes
@@ -225,19 +224,15 @@ __global__ __launch_bounds__(DEC_PARSE_NT) void k_dec_parse(const uint8_t* __res
             *reinterpret_cast<uint4*>(D.codes + dec_code_at(g, gcur * DEC_GRP)) = *reinterpret_cast<const uint4*>(st);
     };
     int64_t bit = master ? 8 : 4;         // bit position, for the sign-bit reader
-    uint32_t baw = 0u, sfw = 0u;          // four bands' ba / sf bytes, stored as words
+    uint32_t bsw = 0u;                    // two bands' ba | sf << 8, stored as a word
     for (int b = 0; b < PAC_NB; ++b) {
         int a = (int)r.read(4);
         if (a) a++;
         const uint32_t sfv = r.read(4);
-        baw |= (uint32_t)a << (8 * (b & 3));
-        sfw |= sfv << (8 * (b & 3));
-        if ((b & 3) == 3 || b == PAC_NB - 1) {   // uniform
-            if (valid) {
-                *reinterpret_cast<uint32_t*>(D.ba + g * DEC_NBP + (b & ~3)) = baw;
-                *reinterpret_cast<uint32_t*>(D.sf + g * DEC_NBP + (b & ~3)) = sfw;
-            }
-            baw = sfw = 0u;
+        bsw |= ((uint32_t)a | (sfv << 8)) << (16 * (b & 1));
+        if ((b & 1) == 1 || b == PAC_NB - 1) {   // uniform
+            if (valid) *reinterpret_cast<uint32_t*>(D.basf + g * DEC_NBP + (b & ~1)) = bsw;
+            bsw = 0u;
         }
         bit += 8;
         if (!__ballot(a != 0)) continue;   // no lane codes the band
@@ -361,12 +356,15 @@ struct PacDecOut {
 // thread-local and the plain frames need no LDS copy of the lines.  A stereo
 // pair's two samples of a frame go out as one 32-bit store.  Barriers hand off
 // LDS only (lds_sync): the code loads and PCM stores stay in flight across
-// them.  BS (block switching on): 40 KB of LDS (FFT scratch, overlap halves,
-// the short frames' lines) and at most 128 VGPRs, 4 waves per SIMD; without
-// it the short and start / stop frames' code is gone: 32 KB and 91 VGPRs, 5
-// waves per SIMD.
+// them.  At most 128 VGPRs: 4 waves per SIMD.  BS (block switching on): 40 KB
+// of LDS (FFT scratch, overlap halves, the short frames' lines); without it
+// the short and start / stop frames' code is gone (32 KB).  Measured: with
+// the field loads of a block sunk by the compiler into "ba != 0" branches
+// (one serial round trip per line), 5 waves per SIMD gave 55.7 M blocks/s;
+// with them forced into one round trip (below) 4 waves give 63.4 M, and 5
+// waves spill (49.8 M).
 template <bool BS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5))) void k_dec_synth(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_dec_synth(
     const PacTables* __restrict__ T, PacDecWork D, const int64_t* __restrict__ cb_base,
     const int64_t* __restrict__ nblk, const int64_t* __restrict__ seg_base, int n_streams, int nch, int master,
     PacDecOut O) {
@@ -388,12 +386,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5)
     // the thread's four lines (pre-twiddle order), their bands and whether a band covers them
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
     auto ln = [&](int i) { const int q = (i >> 1) * 256 + tid; return (i & 1) ? 1023 - 2 * q : 2 * q; };
-    int bnd[4];
+    int bnd0[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bnd[i] = ln(i) < lend ? T->band_of_line[ln(i)] : -1;
+    for (int i = 0; i < 4; ++i) bnd0[i] = ln(i) < lend ? T->band_of_line[ln(i)] : -1;
     for (int c = 0; c < nc; ++c)
         for (int i = tid; i < PAC_HALFN; i += 256) prev[c][i] = 0.0;
     const int64_t base = cb_base[s];
+    const int64_t fos = O.fo[s];                  // once: the stores below may alias it for the compiler
     const PacTables* const T0 = T;
     const int tid0 = tid;
     for (int64_t b = b0 > 0 ? b0 - 1 : 0; b < b1; ++b) {
@@ -402,31 +401,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5)
         // holding them live across the loop (163 -> 123 VGPRs, no spills: 4
         // waves per SIMD instead of 3; decode 48.4 -> 51.3 M blocks/s.  At 3
         // waves the recomputation alone is a loss: 45.4)
-        const PacTables* __restrict__ T = T0;
-        int tid = tid0;
-        asm volatile("" : "+s"(T), "+v"(tid));
+        // (the pointer is offset by an opaque zero, not itself passed through
+        // the asm: it stays a global pointer -- global_load, not flat_load,
+        // whose waits also drain the LDS operations)
+        int zero = 0, tid = tid0;
+        asm volatile("" : "+s"(zero), "+v"(tid));
+        const PacTables* __restrict__ T = T0 + zero;
+        int bnd[4];                                // the bands too (no per-line field pointers kept)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bnd[i] = bnd0[i];
+            asm volatile("" : "+v"(bnd[i]));
+        }
         auto ln = [&](int i) { const int q = (i >> 1) * 256 + tid; return (i & 1) ? 1023 - 2 * q : 2 * q; };
         // vDequantize of the four lines of each channel, / 2^overall (codec.py:25-45)
         // every field loaded unconditionally (a line past the last band reads
         // band 0's and discards it): the loads of a block are one round trip,
         // not ba's and then, under "ba != 0", the scale factor's and code's
         double x[2][4];
+        int fba[2][4], fcd[2][4], fov[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             if (c >= nc) break;
             const int64_t g = base + b * nch + c0 + c;
+            fov[c] = D.overall[g];
+            // uniform bases (scalar registers) + 32-bit lane offsets: no 64-bit
+            // address per load
+            const uint16_t* bsg = D.basf + g * DEC_NBP;
+            const uint16_t* cdg = D.codes + dec_code_at(g, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const unsigned bi = bnd[i] >= 0 ? (unsigned)bnd[i] : 0u;
+                const int l = ln(i);
+                fba[c][i] = bsg[bi];                                // ba | sf << 8
+                fcd[c][i] = cdg[(unsigned)((l / DEC_GRP) * (WAVE * DEC_GRP) + l % DEC_GRP)];
+            }
+        }
+        // every field in registers before any is used: the compiler would
+        // otherwise sink the scale-factor and code loads under "ba != 0" --
+        // a second round trip per line (in the ISA of the 5-wave build)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= nc) break;
+            asm volatile("" ::"v"(fov[c]));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fba[c][i]), "v"(fcd[c][i]));
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= nc) break;
             // / 2^overall as * 2^-overall: a power of two, the same double
             // (the lines are far from the subnormal range), one multiply
             // instead of a division sequence per line
-            const double unscale = __builtin_ldexp(1.0, -(int)D.overall[g]);
+            const double unscale = __builtin_ldexp(1.0, -fov[c]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int bi = bnd[i] >= 0 ? bnd[i] : 0;
-                const int ba0 = D.ba[g * DEC_NBP + bi];
-                const int sf = D.sf[g * DEC_NBP + bi];
-                const int code = D.codes[dec_code_at(g, ln(i))];
-                const int ba = bnd[i] >= 0 ? ba0 : 0;
-                const double v = ba ? pac_dequantize(sf, code, ba) : 0.0;
+                const int ba = bnd[i] >= 0 ? (fba[c][i] & 255) : 0;
+                const double v = ba ? pac_dequantize(fba[c][i] >> 8, fcd[c][i], ba) : 0.0;
                 x[c][i] = v * unscale;
             }
         }
@@ -476,7 +507,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5)
                 const double v = prev[c][i] + w0;
                 prev[c][i] = w1;
                 if (!out) return;
-                const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
+                const int64_t o = (fos + ob * PAC_HALFN + i) * nch + c0 + c;
                 O.pcm[o] = pac_float_to_pcm(v);
                 if (O.fpcm) O.fpcm[o] = v;
             };
@@ -501,7 +532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5)
                     const double v = prev[c][i] + imdct_window_at(U, T, i, 0);
                     prev[c][i] = imdct_window_at(U, T, i + PAC_HALFN, 0);
                     if (!out) continue;
-                    const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * 2;
+                    const int64_t o = (fos + ob * PAC_HALFN + i) * 2;
                     const uint32_t h = (uint16_t)pac_float_to_pcm(v);
                     if (O.fpcm) O.fpcm[o + c] = v;
                     if (c == 0) h0[k] = h;
@@ -514,7 +545,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS ? 4 : 5)
         const int64_t ob = nb - 1 + (O.preroll ? 1 : 0);
         for (int c = 0; c < nc; ++c)
             for (int i = tid; i < PAC_HALFN; i += 256) {
-                const int64_t o = (O.fo[s] + ob * PAC_HALFN + i) * nch + c0 + c;
+                const int64_t o = (fos + ob * PAC_HALFN + i) * nch + c0 + c;
                 O.pcm[o] = pac_float_to_pcm(prev[c][i]);
                 if (O.fpcm) O.fpcm[o] = prev[c][i];
             }

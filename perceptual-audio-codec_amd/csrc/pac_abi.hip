@@ -131,6 +131,10 @@ static void build_tables(int fs, int window, PacTables* t) {
         acc += t->nlines[b];
     }
     for (int l = acc; l < PAC_HALFN; l++) t->band_of_line[l] = PAC_NB - 1;  // unreachable
+    for (int l = 0; l < PAC_HALFN; l++) {
+        const int b = t->band_of_line[l];
+        t->band_span[l] = t->lower[b] | ((t->lower[b] + t->nlines[b] - 1) << 10) | (b << 20);
+    }
     for (int n = 0; n < PAC_N; n++) {
         double tt = (double)n;
         t->sine[n] = sin((tt + 0.5) * M_PI / (double)PAC_N);

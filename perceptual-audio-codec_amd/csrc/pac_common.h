@@ -77,6 +77,10 @@ struct PacTables {
     double2 mdct_post_s[128];         // exp(-i pi q / 256)
     double bark_line_s[256], tiq_s[256], bark_bin_s[256], mld_s[256];
     double pow_kl_s[256], pow_mkl_s[256];   // 2^(KL z_l), 2^(-KL z_l) of the short lines
+    // line l's band b = band_of_line[l] with its span: lower[b] | (lower[b] +
+    // nlines[b] - 1) << 10 | b << 20 (k_master_front: one load per line, at
+    // the kernel's start, instead of lower[b], nlines[b] behind band_of_line)
+    int32_t band_span[PAC_HALFN];
 };
 
 // Huffman tables (Huffman.py, exported by tests/golden/export_huffman_tables.py)

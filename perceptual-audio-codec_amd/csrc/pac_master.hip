@@ -732,13 +732,18 @@ __device__ __forceinline__ void grp_spectrum_cplx2p(const D4& d4, const PacTable
 // reference's transform; rounding of the same class as an FFT's (the terms
 // are bounded by the raw spectrum's bins).  Exactly-zero lines take the
 // reference's signed zero.
-__device__ __forceinline__ double mdct_from_dft(double2 x0, double2 x1, const PacTables* __restrict__ T, int k) {
-    const double4 tw = T->mdct_tw2[k];
+// (tw = T->mdct_tw2[k], zn = T->mdct_zero_neg[k]: the caller may load them
+// ahead; the exact-zero sign applied by a select -- under "r == 0" its load
+// was a branch of its own, which kept the next line's loads behind it)
+__device__ __forceinline__ double mdct_from_dft_tw(double2 x0, double2 x1, double4 tw, int zn) {
     double r = x0.y * tw.x;
     r = __builtin_fma(-x0.x, tw.y, r);
     r = __builtin_fma(-x1.y, tw.z, r);
     r = __builtin_fma(x1.x, tw.w, r);
-    return r == 0.0 ? (T->mdct_zero_neg[k] ? -0.0 : 0.0) : r;
+    return r == 0.0 ? __longlong_as_double((long long)(zn != 0) << 63) : r;
+}
+__device__ __forceinline__ double mdct_from_dft(double2 x0, double2 x1, const PacTables* __restrict__ T, int k) {
+    return mdct_from_dft_tw(x0, x1, T->mdct_tw2[k], T->mdct_zero_neg[k]);
 }
 
 // parity probe (pac_debug_mdct_dft): blocks 2 i, 2 i + 1 of `data` (n blocks
@@ -839,13 +844,23 @@ __device__ __forceinline__ void lrms_block(const PacSource& src, const PacTables
     // after the leaf sums below, so that the lines and the sums are not live
     // together: the kernel's 5 waves per SIMD need <= 96 VGPRs)
     auto mdct_lines = [&]() {
+        // each line's twiddles loaded one line ahead: the next line's round
+        // trip overlaps this line's arithmetic (one exposed round trip, not four)
+        double4 twn = T->mdct_tw2[1023 - tid];
+        int znn = T->mdct_zero_neg[1023 - tid];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = 1023 - 256 * i - tid;
+            const double4 tw = twn;
+            const int zn = znn;
+            if (i < 3) {
+                twn = T->mdct_tw2[k - 256];
+                znn = T->mdct_zero_neg[k - 256];
+            }
             const double2 a0 = bufA[k], b0 = bufB[k];
             const double2 a1 = k == 1023 ? make_double2(nyA, 0.0) : bufA[k + 1];
             const double2 b1 = k == 1023 ? make_double2(nyB, 0.0) : bufB[k + 1];
-            const double xl = mdct_from_dft(a0, a1, T, k), xr = mdct_from_dft(b0, b1, T, k);
+            const double xl = mdct_from_dft_tw(a0, a1, tw, zn), xr = mdct_from_dft_tw(b0, b1, tw, zn);
             if constexpr (CODED) {
                 cl[i] = xl;
                 cr[i] = xr;
@@ -1117,9 +1132,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // band mask, loaded before the MDCT (no wait: the LDS barriers leave them
     // in flight) so that the threshold loads can all issue right after it
     const int lend = T->lower[PAC_NB - 1] + T->nlines[PAC_NB - 1];
-    int bl4[4];
+    int sp4[4];                                   // band | its first and last line (band_span)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bl4[i] = T->band_of_line[i * 256 + tid];
+    for (int i = 0; i < 4; ++i) sp4[i] = T->band_span[i * 256 + tid];
     const uint32_t msm = st ? F.msm[gb] : 0u;     // mono: all L/R
     const uint32_t mldm = st ? F.mldm[gb] : 0u;   // the MLD rows that exist (k_master_thr)
     MPROF(0);
@@ -1183,7 +1198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = i * 256 + tid;
-        ms4[i] = l < lend ? (int)((msm >> bl4[i]) & 1u) : 0;
+        ms4[i] = l < lend ? (int)((msm >> (sp4[i] >> 20)) & 1u) : 0;
         const double* tp = thr + (ms4[i] ? 2 * PAC_HALFN : 0) + l;
         t4[i][0] = tp[0];
         t4[i][1] = tp[PAC_HALFN];
@@ -1234,7 +1249,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int l = i * 256 + tid;
-        const int b = bl4[i];
+        const int b = sp4[i] >> 20;
         const int ms = ms4[i];
         // the coded lines: M/S of the scaled channels, or the scaled L, R
         double v0, v1;
@@ -1275,7 +1290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         // serialise: at most 4 per band and wave)
         const bool in = l < lend;
         const int lane = tid & (WAVE - 1);
-        const int e = in ? min(lane | 15, lane + (T->lower[b] + T->nlines[b] - 1 - l)) : lane;
+        const int e = in ? min(lane | 15, lane + (((sp4[i] >> 10) & 1023) - l)) : lane;
         unsigned long long k0 = in ? (unsigned long long)__double_as_longlong(d0) : 0ull;   // positive: bits order
         unsigned long long k1 = in ? (unsigned long long)__double_as_longlong(d1) : 0ull;
         unsigned long long k2 = in ? (unsigned long long)__double_as_longlong(fabs(v0)) : 0ull;
@@ -1284,7 +1299,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         seg_max_step<2>(k0, k1, k2, k3, lane + 2 <= e);
         seg_max_step<4>(k0, k1, k2, k3, lane + 4 <= e);
         seg_max_step<8>(k0, k1, k2, k3, lane + 8 <= e);
-        if (in && ((lane & 15) == 0 || l == T->lower[b])) {
+        if (in && ((lane & 15) == 0 || l == (sp4[i] & 1023))) {
             atomicMax(&key[0][b], k0);
             atomicMax(&key[1][b], k1);
             atomicMax(&key[2][b], k2);

@@ -87,22 +87,39 @@ __device__ __forceinline__ double sample(const BlockRef& r, int i) {
 }
 
 // The same samples with the stream-edge test hoisted: samples [ilo, ihi) of
-// the block lie inside the stream; p points at sample ilo of channel c.
+// the block lie inside the stream; p points at sample ilo of channel c.  The
+// int16 samples load through a raw buffer resource over exactly those frames
+// (from p): a sample outside them is out of the range and reads 0 -- no
+// per-sample branch (under one, each sample's load was waited on before the
+// next was issued: a serial round trip per sample).
 struct BlockPcm {
     const int16_t* p;
     const double* f;
     int ilo, ihi, nch;
+    __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ explicit BlockPcm(const BlockRef& r) {
         f = r.fsrc;
         nch = r.nch;
-        if (f) { p = nullptr; ilo = 0; ihi = PAC_N; return; }
+        if (f) { p = nullptr; ilo = 0; ihi = PAC_N; rs = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000); return; }
         const int64_t ff = r.first_frame;
         ilo = ff < 0 ? (int)(-ff) : 0;
         const int64_t top = r.n_frames - ff;
         ihi = top < ilo ? ilo : (top > PAC_N ? PAC_N : (int)top);
         p = r.pcm + ((ff + ilo) * r.nch + r.c);
+        rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 2 * (ihi - ilo) * nch, 0x00020000);
+    }
+    // sample i of channel c + u (u: stereo_sample's other channel), 0 outside the stream
+    __device__ __forceinline__ int code(int i, int u = 0) const {
+        return (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rs, 2 * ((i - ilo) * nch + u), 0, 0);
     }
     __device__ __forceinline__ double operator()(int i) const {
+        if (f) return f[i];
+        return pac_pcm_to_float(code(i));
+    }
+    // the same through a plain pointer and a bounds test: for a BlockPcm that
+    // differs between the lanes of a wave (k_bs_attack), whose buffer resource
+    // could not live in scalar registers (a waterfall loop per load)
+    __device__ __forceinline__ double at(int i) const {
         if (f) return f[i];
         int c = 0;
         if (i >= ilo && i < ihi) c = p[(i - ilo) * nch];
@@ -140,9 +157,7 @@ struct StereoFrames {
 // sample i of channel u (0, 1) of a stereo block (r: the channel-0 BlockPcm of
 // an interleaved stereo source): one 16-bit load; zero outside the stream
 __device__ __forceinline__ double stereo_sample(const BlockPcm& r, int i, int u) {
-    int c = 0;
-    if (i >= r.ilo && i < r.ihi) c = r.p[2 * (i - r.ilo) + u];
-    return pac_pcm_to_float(c);
+    return pac_pcm_to_float(r.code(i, u));
 }
 
 // xs[i] = x(i) * sine[i] (window.py:27-39, codec.py:240) into LDS, i < 2048

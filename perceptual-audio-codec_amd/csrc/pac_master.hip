@@ -558,9 +558,9 @@ __global__ __launch_bounds__(64) void k_bs_attack(PacSource src, int64_t nblocks
     double e = 0.0;
     if (live) {
         const BlockPcm r(locate(src, gb, c));
-        double xp = sg ? r(128 * sg - 1) : 0.0;
+        double xp = sg ? r.at(128 * sg - 1) : 0.0;      // per-lane blocks: at(), not the buffer path
         for (int n = 128 * sg; n < 128 * sg + 128; ++n) {
-            const double x = r(n);
+            const double x = r.at(n);
             const double dd = n ? __dsub_rn(x, xp) : 0.0;
             e = __dadd_rn(e, __dmul_rn(dd, dd));
             xp = x;

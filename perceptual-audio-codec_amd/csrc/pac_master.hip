@@ -301,7 +301,8 @@ __device__ __forceinline__ void thr_variant(const PacTables* __restrict__ T, con
 __device__ __forceinline__ void mld_rows_back(int* kept, int tid) {
     lds_sync();
     if (tid == 0)
-        *reinterpret_cast<uint32_t*>(*reinterpret_cast<volatile unsigned long long*>(kept + 2)) = (uint32_t)kept[0];
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(
+            *(volatile __attribute__((address_space(3))) unsigned long long*)(kept + 2)) = (uint32_t)kept[0];   // LDS read, global store
 }
 
 // One workgroup per (block, variant pair) -- {0,1} = L/R, {2,3} = M/S,
@@ -444,7 +445,8 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
     TPROF(8);
     // wave-uniform by construction; readfirstlane makes it scalar for the
     // compiler too, so that the pass below (ballots) runs under no exec mask
-    const unsigned long long pv = *reinterpret_cast<volatile unsigned long long*>(park);
+    typedef volatile __attribute__((address_space(3))) unsigned long long lds_u64;   // an LDS read, not a flat one
+    const unsigned long long pv = *(lds_u64*)park;
     const unsigned long long pbase = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(pv >> 32)) << 32) |
                                      (unsigned)__builtin_amdgcn_readfirstlane((int)pv);
     if (pbase) {
@@ -464,8 +466,12 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int lane = t2 & (WAVE - 1), w = __builtin_amdgcn_readfirstlane(t2 / WAVE);
         const int prow = __builtin_amdgcn_readfirstlane(park[2]);
-        double* blk = reinterpret_cast<double*>(pbase);
-        const unsigned long long* tm = reinterpret_cast<const unsigned long long*>(blk + 2 * PAC_HALFN);
+        // (the parked address cast back to a global pointer: global loads and
+        // stores, not flat ones -- whose waits also drain the LDS operations)
+        typedef __attribute__((address_space(1))) double gdouble;
+        typedef __attribute__((address_space(1))) unsigned long long gu64;
+        gdouble* blk = reinterpret_cast<gdouble*>(pbase);
+        gu64* tm = reinterpret_cast<gu64*>(blk + 2 * PAC_HALFN);
         // the wave's four rows loaded together (one round trip; a row this
         // workgroup did not store is read too -- in bounds, stale -- and ignored)
         constexpr int NQ = 16 / (FRONT_NT / WAVE);
@@ -486,7 +492,7 @@ __global__ __launch_bounds__(FRONT_NT) void k_master_thr(PacSource src, const Pa
             if (__ballot(m[q] > sv[q])) need |= 1u << r;
             if (__ballot(sv[q] > m[q])) need |= 1u << (16 + r);
         }
-        if (lane == 0) MLD_NEED_AT(blk + 5 * PAC_HALFN)[w] = need;
+        if (lane == 0) reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(blk + 6 * PAC_HALFN - 2)[w] = need;   // MLD_NEED_AT
     }
 }
 
